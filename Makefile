@@ -1,0 +1,48 @@
+# Build the MI355X library (HIP, gfx950) and the CPU oracle (test infrastructure).
+#   make            -> real_time_ray_tracer_amd/librtrt.so, oracle/build/librt_oracle.so, build/rt_headless
+#   make lib|oracle|headless|clean
+HIPCC    ?= /opt/rocm/bin/hipcc
+CC       ?= gcc
+ARCH     ?= gfx950
+PKG      := real_time_ray_tracer_amd
+CSRC     := $(PKG)/csrc
+OBJDIR   := build/obj
+
+# -ffp-contract=off + correctly-rounded f32 '/' and sqrt: the float semantics shared with the
+# oracle (oracle/rt_oracle.h).  No fast-math anywhere.
+HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off \
+            -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function -Iinclude
+CFLAGS_ORACLE := -O3 -march=x86-64-v3 -ffp-contract=off -fopenmp -fPIC -std=c99 -Wall
+
+LIB      := $(PKG)/librtrt.so
+ORACLE   := oracle/build/librt_oracle.so
+HEADLESS := build/rt_headless
+
+all: lib oracle headless
+lib: $(LIB)
+oracle: $(ORACLE)
+headless: $(HEADLESS)
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/*.h include/rt/*.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(OBJDIR)/rt_host.o: $(CSRC)/rt_host.cpp include/rt/*.h | $(OBJDIR)
+	$(HIPCC) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude -c $< -o $@
+
+$(LIB): $(OBJDIR)/rt_kernels.o $(OBJDIR)/rt_shim.o $(OBJDIR)/rt_host.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+$(ORACLE): oracle/rt_oracle.c oracle/rt_oracle.h include/rt/layout.h
+	@mkdir -p oracle/build
+	$(CC) $(CFLAGS_ORACLE) -shared -o $@ oracle/rt_oracle.c -lm
+
+$(HEADLESS): $(CSRC)/rt_headless.cpp $(LIB) include/rt/*.h
+	$(CXX) -O2 -std=c++17 -Iinclude -o $@ $< -L$(PKG) -lrtrt -Wl,-rpath,'$$ORIGIN/../$(PKG)'
+
+$(OBJDIR):
+	@mkdir -p $(OBJDIR)
+
+clean:
+	rm -rf build oracle/build $(LIB)
+
+.PHONY: all lib oracle headless clean

@@ -1,0 +1,177 @@
+/*
+ * rt/abi.h — C ABI of the MI355X ray-tracing hot path (librtrt.so).
+ *
+ * Drop-in for the GL dispatch boundary of JustinPrivitera/Real_Time_Ray_Tracer:
+ *   the reference binds one std430 SSBO `shader_data` (resources/p_compute.glsl:28-63) plus
+ *   an rgba32f image (src/main.cpp:389-392) and launches one of five compute programs with
+ *   glDispatchCompute(WIDTH, HEIGHT, 1) from
+ *     Application::compute()              src/main.cpp:553-578
+ *     Application::compute_one_shader()   src/main.cpp:580-620
+ *     Application::compute_two_shaders()  src/main.cpp:622-671
+ *   and packs the scene / rand buffer / light with
+ *     loadShapeBuffer()    src/main.cpp:395-469
+ *     fill_rand_buffer()   src/main.cpp:535-539
+ *     moving_light()       src/main.cpp:541-551
+ *     camera basis         src/main.cpp:772-779
+ *
+ * Every entry point below names the reference function it replaces.  Conventions:
+ *   - plain C types only; no exceptions cross the ABI;
+ *   - return value 0 = RT_OK, < 0 = one of the RT_E* codes (rt_strerror() names it);
+ *     functions that return a frame index return it (>= 0) on success;
+ *   - one rt_ctx per (device, frame strip); a context is not thread-safe;
+ *   - all GPU work is ordered on the context's HIP stream (rt_set_stream to share one).
+ *
+ * Host-only helpers (rt_pack_*, rt_camera_basis, rt_fill_rand_buffer, rt_moving_light,
+ * rt_scenegen, rt_init_scene, rt_strerror, rt_version) never touch the GPU.
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "layout.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------- */
+enum {
+  RT_OK = 0,
+  RT_E_INVAL = -1,    /* bad argument (size, index, mode, program ...) */
+  RT_E_NOMEM = -2,    /* host or device allocation failed */
+  RT_E_HIP = -3,      /* a HIP runtime call failed; rt_last_hip_error() has the code */
+  RT_E_NODEV = -4,    /* no HIP device / bad device ordinal */
+  RT_E_STATE = -5     /* call order (e.g. dispatch before a header was uploaded) */
+};
+
+/* ---- compute programs (src/main.cpp:484-501, resources/<shader>.glsl) ------------------ */
+enum {
+  RT_PROG_AOP_COMPUTE = 1,        /* resources/aop_compute.glsl        (mode 1 pass 1) */
+  RT_PROG_AOP_POSTPROCESSING = 2, /* resources/aop_postprocessing.glsl (mode 1 pass 2) */
+  RT_PROG_AO_COMPUTE = 3,         /* resources/ao_compute.glsl         (mode 2)        */
+  RT_PROG_P_COMPUTE = 4,          /* resources/p_compute.glsl          (mode 3)        */
+  RT_PROG_H_COMPUTE = 5,          /* resources/h_compute.glsl          (mode 4)        */
+  RT_PROG_COUNT = 6
+};
+
+/* ---- lighting modes (`mycam.lighting`, src/main.cpp:266-273, 553-578) -------------- */
+enum { RT_MODE_AO_PP = 1, RT_MODE_AO = 2, RT_MODE_PHONG = 3, RT_MODE_PHONG_REFL = 4 };
+
+typedef struct rt_ctx rt_ctx;
+
+typedef struct {
+  int width;      /* WIDTH  (src/main.cpp:29): full-frame width in pixels               */
+  int height;     /* HEIGHT (src/main.cpp:30): full-frame height in pixels              */
+  int num_shapes; /* NUM_SHAPES (src/main.cpp:34): capacity of simple_shapes[S][5]      */
+  int spp;        /* AA (src/main.cpp:31): samples per pixel; rand_buffer has 2*spp vec4 */
+  int num_frames; /* NUM_FRAMES (src/main.cpp:36): g-buffer ring length, normally 8     */
+  int max_depth;  /* RECURSION_DEPTH (resources/ao_compute.glsl:10): path length cap, 20 */
+  int row_begin;  /* this context renders frame rows [row_begin, row_end);              */
+  int row_end;    /*   row_begin = row_end = 0 means the whole frame                    */
+} rt_config;
+
+/* ---- context lifetime ------------------------------------------------------------- */
+/* Replaces computeInitGeom()/computeInit() (src/main.cpp:471-501): allocates the device-
+ * resident header, g-buffer ring (zeroed like the value-initialised ssbo_CPUMEM) and image. */
+int rt_create(int device, const rt_config* cfg, rt_ctx** out);
+int rt_destroy(rt_ctx* ctx);
+/* Order all of the context's work on an external HIP stream (hipStream_t); NULL restores the
+ * context's own stream. */
+int rt_set_stream(rt_ctx* ctx, void* hip_stream);
+void* rt_get_stream(rt_ctx* ctx);
+int rt_synchronize(rt_ctx* ctx);
+int rt_last_hip_error(rt_ctx* ctx);
+
+/* ---- device-resident path (what render() drives each frame) ------------------------ */
+/* Upload the SSBO prefix: 7 header vec4 + simple_shapes[S][5] + rand_buffer[2*spp],
+ * byte-identical to the reference's std430 layout (bytes == rt_header_bytes(S, spp)).
+ * Replaces the memcpy-in of src/main.cpp:598-602 for everything but the g-buffer. */
+int rt_upload_header(rt_ctx* ctx, const void* header, size_t bytes);
+/* Replace only rand_buffer[2*spp] (fill_rand_buffer, src/main.cpp:535-539); n_vec4 == 2*spp. */
+int rt_upload_rand_buffer(rt_ctx* ctx, const float* rand_vec4, size_t n_vec4);
+/* Run one program on frame slot `frame` (glDispatchCompute(W,H,1), src/main.cpp:604). */
+int rt_run_program(rt_ctx* ctx, int program, int frame);
+/* compute() (src/main.cpp:553-578) without the host-side light/rand updates:
+ * mode 1 = aop_compute + aop_postprocessing, 2 = ao_compute, 3 = p_compute, 4 = h_compute.
+ * Returns the next frame slot (frame+1) % num_frames, as compute_one_shader does. */
+int rt_dispatch(rt_ctx* ctx, int mode, int frame);
+/* Copy device state to the host in the REFERENCE layout.  Any pointer may be NULL.
+ * pixels/normals/depth: [F][W][R] vec4 (x-major, y fastest; R = rows of this context),
+ * image: [R][W] rgba32f (row 0 = row_begin, bottom-left origin like the GL texture). */
+int rt_download(rt_ctx* ctx, float* pixels, float* normals, float* depth, float* image);
+/* Upload a reference-layout g-buffer ring ([F][W][R] vec4 each; NULL = leave as is). */
+int rt_upload_gbuffer(rt_ctx* ctx, const float* pixels, const float* normals, const float* depth);
+/* Device pointer of the context's image ([R][W] float4), for collectives. */
+void* rt_image_device_ptr(rt_ctx* ctx);
+/* Render the image into a caller-owned device buffer of R*W float4 (NULL = own buffer). */
+int rt_bind_image(rt_ctx* ctx, void* device_ptr);
+
+/* ---- host-buffer parity path (mirrors the reference call shape) -------------------- */
+/* compute_one_shader(frame_num, prog) (src/main.cpp:580-620): sets mode.y = frame_num in
+ * `ssbo` (a whole ssbo_data-layout host buffer of rt_ssbo_bytes(S,spp,W,R,F) bytes), copies
+ * it in, runs `program`, copies the g-buffer back into `ssbo`, writes the image if non-NULL,
+ * and returns (frame_num + 1) % F. */
+int rt_compute_one_shader(rt_ctx* ctx, void* ssbo, int frame_num, int program, float* image);
+/* compute_two_shaders(frame_num, p1, p2) (src/main.cpp:622-671). */
+int rt_compute_two_shaders(rt_ctx* ctx, void* ssbo, int frame_num, int program1, int program2,
+                           float* image);
+
+/* ---- instrumentation --------------------------------------------------------------- */
+/* When on, every kernel launch is bracketed by HIP events on the context stream. */
+int rt_enable_timing(rt_ctx* ctx, int on);
+/* Sum of event-measured durations of `program`'s kernel since the last reset. */
+int rt_kernel_stats(rt_ctx* ctx, int program, int* launches, double* total_ms);
+int rt_reset_stats(rt_ctx* ctx);
+
+/* ---- device math self-test (parity of the shared float semantics) ------------------ */
+enum {
+  RT_MATH_SIN = 0,       /* deterministic sin used by random() (in: x)                 */
+  RT_MATH_RANDOM = 1,    /* random(vec2) hash, p_compute.glsl:65-75 (in: x,y pairs)    */
+  RT_MATH_SQRT = 2,      /* IEEE sqrtf (in: x)                                         */
+  RT_MATH_DIV = 3,       /* IEEE a/b (in: a,b pairs)                                   */
+  RT_MATH_NORMALIZE = 4, /* normalize(vec3) (in: xyz triples, out: xyz triples)        */
+  RT_MATH_SPHERE = 5     /* sphere_eval_ray (in: pos3,dir3,center3,r = 10 floats)      */
+};
+int rt_selftest_math(rt_ctx* ctx, int fn, const float* in, float* out, size_t n);
+
+/* ---- host-only scene / header helpers (no GPU) ------------------------------------- */
+/* loadShapeBuffer() entries (src/main.cpp:417-420, 439-442, 462-466).  `header` is the
+ * SSBO prefix as float*, S its shape capacity; index i < S.  Unwritten lanes are untouched,
+ * as in the reference. */
+int rt_pack_sphere(float* header, int S, int i, const float center[3], float radius,
+                   const float color[3], float reflectivity, int emissive);
+/* plane(normal, dist, color) — p0 = dist * normal (src/geom_objs/plane.h:31-34). */
+int rt_pack_plane(float* header, int S, int i, const float normal[3], float dist,
+                  const float color[3], float reflectivity, int emissive);
+int rt_pack_rectangle(float* header, int S, int i, const float llc[3], const float right[3],
+                      const float up[3], const float color[3], float reflectivity, int emissive);
+/* Camera basis of render() (src/main.cpp:772-779): w = look; u = normalize(cross(up,w));
+ * v = normalize(cross(w,u)); horizontal = aspect*u; vertical = v;
+ * llc_minus_campos = -0.5*(horizontal+vertical) - w; writes those + camera_location. */
+int rt_camera_basis(float* header, const float location[3], const float up[3],
+                    const float look_towards[3], float aspect);
+/* Header fill of compute_one_shader (src/main.cpp:584-589): mode.y = frame, mode.z = n. */
+int rt_set_mode(float* header, int frame, int num_objects);
+/* fill_rand_buffer (src/main.cpp:535-539) with a seeded generator instead of rand():
+ * splitmix64(seed), top 24 bits / 2^24 per float, 2*AA vec4. */
+int rt_fill_rand_buffer(float* header, int S, int AA, uint64_t seed);
+/* moving_light (src/main.cpp:541-551). */
+int rt_moving_light(float* header, int light_movement);
+/* Synthetic seeded scene of SURVEY §8d: ground sphere + (n_objects-1) random spheres, the
+ * default camera (src/main.cpp:98-100), light (-12,8,7), SKY background, mode.z = n_objects.
+ * S = capacity >= n_objects. */
+int rt_scenegen(float* header, int S, int n_objects, int AA, uint64_t seed, float aspect);
+/* The reference's built-in scenes 1, 5, 6 (src/scene.h:15-167) with the default camera. */
+int rt_init_scene(float* header, int S, int AA, int which, float aspect);
+
+const char* rt_strerror(int status);
+int rt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_ABI_H */

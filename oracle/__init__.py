@@ -1,0 +1,98 @@
+"""ctypes wrapper of the CPU oracle (oracle/rt_oracle.c).  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this package,
+and only as the checker / CPU baseline — never as the product path.
+Parity unpinned by reference artifacts (the reference has none); see rt_oracle.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "build" / "librt_oracle.so"
+
+AOP_COMPUTE, AOP_POSTPROCESSING, AO_COMPUTE, P_COMPUTE, H_COMPUTE = 1, 2, 3, 4, 5
+
+
+class rto_dims(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ("W", "H", "S", "AA", "F", "D", "gy0", "gh")]
+
+
+_lib = None
+
+
+def build():
+    """Compile the oracle with gcc (Makefile target `oracle`)."""
+    subprocess.run(["make", "-s", "oracle"], cwd=HERE.parent, check=True)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        build()
+    lib = C.CDLL(str(LIB_PATH))
+    fp = C.POINTER(C.c_float)
+    lib.rto_run_program.argtypes = [fp, C.POINTER(rto_dims), C.c_int, C.c_int, fp, C.c_int, C.c_int, C.c_int]
+    lib.rto_run_program.restype = C.c_int
+    lib.rto_dispatch.argtypes = [fp, C.POINTER(rto_dims), C.c_int, C.c_int, fp, C.c_int]
+    lib.rto_dispatch.restype = C.c_int
+    lib.rto_sin.argtypes = [C.c_float]
+    lib.rto_sin.restype = C.c_float
+    lib.rto_random.argtypes = [C.c_float, C.c_float]
+    lib.rto_random.restype = C.c_float
+    lib.rto_sphere_eval.argtypes = [fp, fp, fp, C.c_float]
+    lib.rto_sphere_eval.restype = C.c_float
+    lib.rto_normalize3.argtypes = [fp, fp]
+    lib.rto_normalize3.restype = None
+    _lib = lib
+    return lib
+
+
+def _fp(a):
+    if a is None:
+        return None
+    assert a.dtype == np.float32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def dims(W, H, S, AA, F=8, D=20, gy0=0, gh=None) -> rto_dims:
+    return rto_dims(W, H, S, AA, F, D, gy0, H if gh is None else gh)
+
+
+def run_program(ssbo: np.ndarray, d: rto_dims, program: int, frame: int, image=None, y0=None, y1=None,
+                nthreads: int = 0) -> None:
+    y0 = d.gy0 if y0 is None else y0
+    y1 = d.gy0 + d.gh if y1 is None else y1
+    rc = load().rto_run_program(_fp(ssbo), C.byref(d), program, frame, _fp(image), y0, y1, nthreads)
+    if rc != 0:
+        raise ValueError(f"rto_run_program rejected its arguments (program {program})")
+
+
+def dispatch(ssbo: np.ndarray, d: rto_dims, mode: int, frame: int, image=None, nthreads: int = 0) -> int:
+    rc = load().rto_dispatch(_fp(ssbo), C.byref(d), mode, frame, _fp(image), nthreads)
+    if rc < 0:
+        raise ValueError(f"rto_dispatch rejected its arguments (mode {mode})")
+    return rc
+
+
+# ---- primitives (vectorised over numpy inputs) --------------------------------------
+def det_sin(x: np.ndarray) -> np.ndarray:
+    f = load().rto_sin
+    return np.array([f(float(v)) for v in np.asarray(x, np.float32).ravel()], np.float32)
+
+
+def random2(xy: np.ndarray) -> np.ndarray:
+    f = load().rto_random
+    xy = np.asarray(xy, np.float32).reshape(-1, 2)
+    return np.array([f(float(a), float(b)) for a, b in xy], np.float32)
+
+
+def nthreads_default() -> int:
+    return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))

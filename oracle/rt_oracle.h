@@ -1,0 +1,71 @@
+/*
+ * rt_oracle.h — CPU restatement of the reference's GLSL hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this code,
+ * and only as the checker / CPU baseline.  The product path (real_time_ray_tracer_amd) never
+ * calls it and fails loudly when its HIP library is missing.
+ *
+ * PARITY STATUS: parity unpinned by reference artifacts.  The reference ships no tests, no
+ * golden images and no fixtures, and it cannot run here (OpenGL 4.3+ compute
+ * with GLFW/GLM and a display).  This restatement is pinned instead by
+ * (1) analytic known-answer tests (tests/test_oracle_kat.py), (2) an independent numpy
+ * restatement (oracle/numpy_ref.py) compared on small frames, and (3) golden fixtures produced
+ * by this file and committed under tests/golden/ (tests/golden/make_golden.py).
+ *
+ * Float semantics (the "GLSL math" both this file and the HIP kernels implement):
+ *   - IEEE binary32 with round-to-nearest, denormals kept, NO implicit contraction
+ *     (built with -ffp-contract=off); operations in the written GLSL order;
+ *   - dot(a,b) = fmaf(a.z,b.z, fmaf(a.y,b.y, a.x*b.x)) (a fused chain, as GLSL compilers emit);
+ *   - sphere discriminant = fmaf(r, r, fmaf(b, b, -dot(pmc,pmc)));
+ *   - normalize(v) = v / sqrtf(dot(v,v)), length(v) = sqrtf(dot(v,v)), IEEE / and sqrtf;
+ *   - sin() inside random() = rto_sin(): float -> double, Cody-Waite reduction by pi/2 and
+ *     fdlibm kernel polynomials evaluated with explicit fma, rounded to float — a
+ *     deterministic, correctly-rounded-in-practice sin both sides can reproduce bit for bit;
+ *   - shadow_ray's `double t` and its dvec3 length run in binary64 (p_compute.glsl:147-163);
+ *   - pow() = libm powf (outputs only; never feeds control flow), so pixels agree within
+ *     the north-star tolerance |g-c| <= 1e-4*max(|g|,|c|) + 1e-6, not bit for bit.
+ */
+#ifndef RT_ORACLE_H
+#define RT_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  int W, H;      /* full frame (WIDTH, HEIGHT): ray generation and post-process bounds */
+  int S;         /* simple_shapes capacity (NUM_SHAPES) */
+  int AA;        /* samples per pixel */
+  int F;         /* NUM_FRAMES */
+  int D;         /* RECURSION_DEPTH */
+  int gy0, gh;   /* g-buffer covers rows [gy0, gy0+gh); full frame: 0, H */
+} rto_dims;
+
+/* programs, same numbering as include/rt/abi.h */
+enum { RTO_AOP_COMPUTE = 1, RTO_AOP_POSTPROCESSING = 2, RTO_AO_COMPUTE = 3,
+       RTO_P_COMPUTE = 4, RTO_H_COMPUTE = 5 };
+
+/* Run `program` over frame rows [y0, y1) (must lie inside the g-buffer rows) on the reference-
+ * layout buffer `ssbo` (header + shapes + rand + pixels/normals/depth [F][W][gh]).  `frame` is
+ * written into mode.y first.  image (optional) is [gh][W] rgba32f, row 0 = gy0.
+ * nthreads <= 0: OpenMP default.  Returns 0 or -1 on bad arguments. */
+int rto_run_program(float* ssbo, const rto_dims* d, int program, int frame, float* image,
+                    int y0, int y1, int nthreads);
+
+/* compute() of src/main.cpp:553-578 for modes 1..4 over the whole g-buffer band; returns the
+ * next frame slot. */
+int rto_dispatch(float* ssbo, const rto_dims* d, int mode, int frame, float* image, int nthreads);
+
+/* primitives (exported for the math self-tests) */
+float rto_sin(float x);
+float rto_random(float x, float y);
+float rto_sphere_eval(const float pos[3], const float dir[3], const float center[3], float r);
+void rto_normalize3(const float v[3], float out[3]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,46 @@
+// rt_kernels.h — launch interface between the C-ABI shim and the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace rt {
+
+constexpr int kMaxFrames = 16;
+
+// Everything one program launch needs.  Passed by value as the kernel argument (lives in the
+// kernarg segment -> SGPRs).  Row ranges are in frame coordinates (row 0 = bottom row).
+struct FrameParams {
+  int W, H;                  // full frame (WIDTH, HEIGHT)
+  int trace_row0, trace_rows;  // rows this launch computes
+  int band_row0, band_rows;  // rows held by the g-buffer ring (strip + halo)
+  int img_row0, img_rows;    // rows of the image (the strip, no halo)
+  int nobj;                  // int(mode.z)
+  int S;                     // stride of the compact shape table (capacity)
+  int spp, D, F, frame;
+  float hx, hy, hz;          // horizontal
+  float vx, vy, vz;          // vertical
+  float lx, ly, lz;          // llc_minus_campos
+  float cx, cy, cz;          // camera_location
+  float Lx, Ly, Lz;          // light_pos
+  float4 bg;                 // background
+  const float4* shapes;      // compact table [4][S]: geo, geo2, col, aux (rt_device.h)
+  const float4* rb;          // rand_buffer[2*spp]
+  float4* out_pix;           // colour destination [band_rows][W]
+  float4* nrm;               // normals_buffer slot `frame` [band_rows][W]
+  float4* dep;               // depth_buffer slot `frame`
+  float4* image;             // [img_rows][W] or nullptr
+  const float4* raw;         // post-process input (pre-filter snapshot of slot `frame`)
+  const float4* hist_pix[kMaxFrames];  // per slot
+  const float4* hist_nrm[kMaxFrames];
+  const float4* hist_dep[kMaxFrames];
+};
+
+enum KernelId { K_AOP = 1, K_POST = 2, K_AO = 3, K_PHONG = 4, K_HYBRID = 5 };
+
+// Launch `program` (RT_PROG_* numbering) on `stream`.  all_spheres selects the specialised
+// intersection loop.  Returns hipSuccess or the launch error.
+hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, hipStream_t stream);
+
+// Device math self-test (rt_selftest_math).
+hipError_t launch_selftest(int fn, const float* d_in, float* d_out, size_t n, hipStream_t stream);
+
+}  // namespace rt

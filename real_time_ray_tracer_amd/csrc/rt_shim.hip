@@ -1,0 +1,578 @@
+// rt_shim.hip — C-ABI host shim (include/rt/abi.h) over the gfx950 kernels.
+//
+// Replaces the GL boundary of src/main.cpp:
+//   computeInitGeom / computeInit (471-501)   -> rt_create
+//   compute_one_shader (580-620)              -> rt_compute_one_shader / rt_run_program
+//   compute_two_shaders (622-671)             -> rt_compute_two_shaders
+//   compute() (553-578)                       -> rt_dispatch
+// Device layout: the g-buffer ring stays resident in HBM as per-slot row-major [rows][W]
+// float4 arrays (pixels has one spare slot buffer so the post-process can write out of
+// place and swap), instead of the reference's 2 x 55.76 MB host round trip per frame.  The
+// reference [F][W][H] layout is produced only by rt_download / consumed by rt_upload_gbuffer.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <utility>
+#include <vector>
+
+#include "../../include/rt/abi.h"
+#include "rt_kernels.h"
+
+namespace {
+
+constexpr int kMaxShapes = 2048;
+constexpr int kMaxSpp = 256;
+constexpr int kStageSlots = 8;
+
+struct Stage {
+  void* host = nullptr;  // pinned
+  size_t bytes = 0;
+  hipEvent_t done = nullptr;
+  bool used = false;
+};
+
+}  // namespace
+
+struct rt_ctx {
+  int device = 0;
+  rt_config cfg{};
+  int own0 = 0, own_rows = 0;    // strip rows
+  int band0 = 0, band_rows = 0;  // strip + 1-row halo (post-process neighbours)
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  float4* d_shapes = nullptr;  // [4][S]
+  float4* d_rb = nullptr;      // [2*spp]
+  std::vector<float4*> pix;    // F+1 buffers
+  std::vector<int> pix_slot;   // slot -> buffer index
+  int spare = 0;
+  std::vector<float4*> nrm, dep;
+  float4* d_image_own = nullptr;
+  float4* d_image = nullptr;
+  std::vector<float> header;   // host copy of the SSBO prefix
+  std::vector<float4> table;   // host compact shape table
+  bool have_header = false;
+  bool all_spheres = true;
+  int nobj = 0;
+  Stage stage[kStageSlots];
+  int stage_next = 0;
+  // timing
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[RT_PROG_COUNT];
+  std::vector<hipEvent_t> event_pool;
+  double total_ms[RT_PROG_COUNT] = {};
+  int launches[RT_PROG_COUNT] = {};
+  int last_hip = 0;
+};
+
+namespace {
+
+int hip_fail(rt_ctx* c, hipError_t e) {
+  if (c) c->last_hip = (int)e;
+  return RT_E_HIP;
+}
+
+#define RT_HIP(ctx, expr)                     \
+  do {                                        \
+    hipError_t _e = (expr);                   \
+    if (_e != hipSuccess) return hip_fail(ctx, _e); \
+  } while (0)
+
+size_t slot_elems(const rt_ctx* c) { return (size_t)c->band_rows * c->cfg.width; }
+
+hipEvent_t get_event(rt_ctx* c) {
+  if (!c->event_pool.empty()) {
+    hipEvent_t e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Async H2D copy through a ring of pinned staging buffers, so callers may reuse their
+// (pageable) memory as soon as the call returns and the stream never has to drain.
+int staged_copy(rt_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (bytes == 0) return RT_OK;
+  Stage& s = c->stage[c->stage_next];
+  c->stage_next = (c->stage_next + 1) % kStageSlots;
+  if (s.used) RT_HIP(c, hipEventSynchronize(s.done));
+  if (s.bytes < bytes) {
+    if (s.host) RT_HIP(c, hipHostFree(s.host));
+    s.host = nullptr;
+    RT_HIP(c, hipHostMalloc(&s.host, bytes, hipHostMallocDefault));
+    s.bytes = bytes;
+  }
+  if (!s.done) RT_HIP(c, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  std::memcpy(s.host, src, bytes);
+  RT_HIP(c, hipMemcpyAsync(dst, s.host, bytes, hipMemcpyHostToDevice, c->stream));
+  RT_HIP(c, hipEventRecord(s.done, c->stream));
+  s.used = true;
+  return RT_OK;
+}
+
+void free_all(rt_ctx* c) {
+  for (auto& s : c->stage) {
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.host) (void)hipHostFree(s.host);
+  }
+  for (int k = 0; k < RT_PROG_COUNT; ++k)
+    for (auto& pr : c->pending[k]) {
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+  for (auto e : c->event_pool) (void)hipEventDestroy(e);
+  for (auto p : c->pix) if (p) (void)hipFree(p);
+  for (auto p : c->nrm) if (p) (void)hipFree(p);
+  for (auto p : c->dep) if (p) (void)hipFree(p);
+  if (c->d_image_own) (void)hipFree(c->d_image_own);
+  if (c->d_shapes) (void)hipFree(c->d_shapes);
+  if (c->d_rb) (void)hipFree(c->d_rb);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+}
+
+const float* hv(const rt_ctx* c, int v) { return c->header.data() + 4 * v; }
+
+void fill_params(const rt_ctx* c, int frame, rt::FrameParams& p) {
+  std::memset(&p, 0, sizeof(p));
+  p.W = c->cfg.width;
+  p.H = c->cfg.height;
+  p.band_row0 = c->band0;
+  p.band_rows = c->band_rows;
+  p.img_row0 = c->own0;
+  p.img_rows = c->own_rows;
+  p.nobj = c->nobj;
+  p.S = c->cfg.num_shapes;
+  p.spp = c->cfg.spp;
+  p.D = c->cfg.max_depth;
+  p.F = c->cfg.num_frames;
+  p.frame = frame;
+  const float *h = hv(c, RT_HDR_HORIZONTAL), *v = hv(c, RT_HDR_VERTICAL),
+              *l = hv(c, RT_HDR_LLC_MINUS_CAMPOS), *cam = hv(c, RT_HDR_CAMERA_LOCATION),
+              *L = hv(c, RT_HDR_LIGHT_POS), *bg = hv(c, RT_HDR_BACKGROUND);
+  p.hx = h[0]; p.hy = h[1]; p.hz = h[2];
+  p.vx = v[0]; p.vy = v[1]; p.vz = v[2];
+  p.lx = l[0]; p.ly = l[1]; p.lz = l[2];
+  p.cx = cam[0]; p.cy = cam[1]; p.cz = cam[2];
+  p.Lx = L[0]; p.Ly = L[1]; p.Lz = L[2];
+  p.bg = make_float4(bg[0], bg[1], bg[2], bg[3]);
+  p.shapes = c->d_shapes;
+  p.rb = c->d_rb;
+  p.image = c->d_image;
+  for (int s = 0; s < c->cfg.num_frames; ++s) {
+    p.hist_pix[s] = c->pix[c->pix_slot[s]];
+    p.hist_nrm[s] = c->nrm[s];
+    p.hist_dep[s] = c->dep[s];
+  }
+  p.nrm = c->nrm[frame];
+  p.dep = c->dep[frame];
+}
+
+int launch(rt_ctx* c, int program, const rt::FrameParams& p) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->timing) {
+    e0 = get_event(c);
+    e1 = get_event(c);
+    if (!e0 || !e1) return RT_E_HIP;
+    RT_HIP(c, hipEventRecord(e0, c->stream));
+  }
+  hipError_t e = rt::launch_program(program, p, c->all_spheres, c->stream);
+  if (e != hipSuccess) return hip_fail(c, e);
+  if (c->timing) {
+    RT_HIP(c, hipEventRecord(e1, c->stream));
+    c->pending[program].emplace_back(e0, e1);
+  }
+  return RT_OK;
+}
+
+int run_program(rt_ctx* c, int program, int frame) {
+  if (!c->have_header) return RT_E_STATE;
+  if (frame < 0 || frame >= c->cfg.num_frames) return RT_E_INVAL;
+  RT_HIP(c, hipSetDevice(c->device));
+  rt::FrameParams p;
+  fill_params(c, frame, p);
+  switch (program) {
+    case RT_PROG_P_COMPUTE:
+    case RT_PROG_H_COMPUTE:
+      // pixels of the strip rows only; the halo rows' pixels are never read
+      p.trace_row0 = c->own0;
+      p.trace_rows = c->own_rows;
+      p.out_pix = c->pix[c->pix_slot[frame]];
+      return launch(c, program, p);
+    case RT_PROG_AO_COMPUTE:
+    case RT_PROG_AOP_COMPUTE:
+      // g-buffer writers trace the halo rows too, so a strip's ring evolves exactly like the
+      // same rows of a whole-frame ring (post-process neighbours + stale-depth reads)
+      p.trace_row0 = c->band0;
+      p.trace_rows = c->band_rows;
+      p.out_pix = c->pix[c->pix_slot[frame]];
+      if (program == RT_PROG_AOP_COMPUTE) p.image = nullptr;  // aop_compute.glsl has no image
+      return launch(c, program, p);
+    case RT_PROG_AOP_POSTPROCESSING: {
+      p.trace_row0 = c->own0;
+      p.trace_rows = c->own_rows;
+      p.raw = c->pix[c->pix_slot[frame]];
+      p.out_pix = c->pix[c->spare];
+      int rc = launch(c, program, p);
+      if (rc != RT_OK) return rc;
+      std::swap(c->pix_slot[frame], c->spare);  // filtered buffer becomes slot `frame`
+      return RT_OK;
+    }
+    default:
+      return RT_E_INVAL;
+  }
+}
+
+int resolve_timing(rt_ctx* c) {
+  bool any = false;
+  for (int k = 0; k < RT_PROG_COUNT; ++k) any = any || !c->pending[k].empty();
+  if (!any) return RT_OK;
+  RT_HIP(c, hipStreamSynchronize(c->stream));
+  for (int k = 0; k < RT_PROG_COUNT; ++k) {
+    for (auto& pr : c->pending[k]) {
+      float ms = 0.0f;
+      RT_HIP(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+      c->total_ms[k] += ms;
+      c->launches[k] += 1;
+      c->event_pool.push_back(pr.first);
+      c->event_pool.push_back(pr.second);
+    }
+    c->pending[k].clear();
+  }
+  return RT_OK;
+}
+
+// device slot [band_rows][W] float4 (own rows) <-> reference [W][R] vec4
+void dev_to_ref(const rt_ctx* c, const float* slot, float* ref) {
+  const int W = c->cfg.width, R = c->own_rows, r0 = c->own0 - c->band0;
+  for (int x = 0; x < W; ++x)
+    for (int r = 0; r < R; ++r)
+      std::memcpy(ref + ((size_t)x * R + r) * 4, slot + ((size_t)(r0 + r) * W + x) * 4, 16);
+}
+void ref_to_dev(const rt_ctx* c, const float* ref, float* slot) {
+  const int W = c->cfg.width, R = c->own_rows, r0 = c->own0 - c->band0;
+  for (int x = 0; x < W; ++x)
+    for (int r = 0; r < R; ++r)
+      std::memcpy(slot + ((size_t)(r0 + r) * W + x) * 4, ref + ((size_t)x * R + r) * 4, 16);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_version(void) { return RT_ABI_VERSION; }
+
+const char* rt_strerror(int s) {
+  switch (s) {
+    case RT_OK: return "ok";
+    case RT_E_INVAL: return "invalid argument";
+    case RT_E_NOMEM: return "out of memory";
+    case RT_E_HIP: return "HIP runtime error";
+    case RT_E_NODEV: return "no HIP device";
+    case RT_E_STATE: return "bad call order";
+    default: return "unknown status";
+  }
+}
+
+int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
+  if (!cfg || !out) return RT_E_INVAL;
+  *out = nullptr;
+  rt_config c = *cfg;
+  if (c.num_frames == 0) c.num_frames = RT_NUM_FRAMES;
+  if (c.max_depth == 0) c.max_depth = RT_RECURSION_DEPTH;
+  if (c.row_begin == 0 && c.row_end == 0) c.row_end = c.height;
+  if (c.width <= 0 || c.height <= 0 || c.num_shapes < 0 || c.num_shapes > kMaxShapes || c.spp <= 0 ||
+      c.spp > kMaxSpp || c.num_frames <= 0 || c.num_frames > rt::kMaxFrames || c.max_depth <= 0 ||
+      c.row_begin < 0 || c.row_end > c.height || c.row_begin >= c.row_end)
+    return RT_E_INVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_E_NODEV;
+  if (device < 0 || device >= ndev) return RT_E_NODEV;
+  rt_ctx* x = new (std::nothrow) rt_ctx();
+  if (!x) return RT_E_NOMEM;
+  x->device = device;
+  x->cfg = c;
+  x->own0 = c.row_begin;
+  x->own_rows = c.row_end - c.row_begin;
+  x->band0 = std::max(0, c.row_begin - 1);
+  x->band_rows = std::min(c.height, c.row_end + 1) - x->band0;
+  int rc = RT_OK;
+  auto fail = [&](hipError_t e) {
+    x->last_hip = (int)e;
+    rc = (e == hipErrorOutOfMemory) ? RT_E_NOMEM : RT_E_HIP;
+  };
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->own_stream, hipStreamNonBlocking);
+  x->stream = x->own_stream;
+  const size_t slot = slot_elems(x) * sizeof(float4);
+  const int F = c.num_frames;
+  if (e == hipSuccess) {
+    x->pix.assign(F + 1, nullptr);
+    x->nrm.assign(F, nullptr);
+    x->dep.assign(F, nullptr);
+    for (int k = 0; k <= F && e == hipSuccess; ++k) e = hipMalloc(&x->pix[k], slot);
+    for (int k = 0; k < F && e == hipSuccess; ++k) e = hipMalloc(&x->nrm[k], slot);
+    for (int k = 0; k < F && e == hipSuccess; ++k) e = hipMalloc(&x->dep[k], slot);
+    // value-initialised ssbo_CPUMEM: the ring starts at zero
+    for (int k = 0; k <= F && e == hipSuccess; ++k) e = hipMemsetAsync(x->pix[k], 0, slot, x->stream);
+    for (int k = 0; k < F && e == hipSuccess; ++k) e = hipMemsetAsync(x->nrm[k], 0, slot, x->stream);
+    for (int k = 0; k < F && e == hipSuccess; ++k) e = hipMemsetAsync(x->dep[k], 0, slot, x->stream);
+  }
+  if (e == hipSuccess) e = hipMalloc(&x->d_image_own, (size_t)x->own_rows * c.width * sizeof(float4));
+  if (e == hipSuccess) e = hipMemsetAsync(x->d_image_own, 0, (size_t)x->own_rows * c.width * sizeof(float4), x->stream);
+  if (e == hipSuccess) e = hipMalloc(&x->d_shapes, (size_t)4 * std::max(1, c.num_shapes) * sizeof(float4));
+  if (e == hipSuccess) e = hipMalloc(&x->d_rb, (size_t)2 * c.spp * sizeof(float4));
+  if (e == hipSuccess) e = hipStreamSynchronize(x->stream);
+  if (e != hipSuccess) {
+    fail(e);
+    free_all(x);
+    delete x;
+    return rc;
+  }
+  x->d_image = x->d_image_own;
+  x->pix_slot.resize(F);
+  for (int k = 0; k < F; ++k) x->pix_slot[k] = k;
+  x->spare = F;
+  x->header.assign(rt_header_bytes(c.num_shapes, c.spp) / 4, 0.0f);
+  x->table.assign((size_t)4 * std::max(1, c.num_shapes), make_float4(0, 0, 0, 0));
+  *out = x;
+  return RT_OK;
+}
+
+int rt_destroy(rt_ctx* c) {
+  if (!c) return RT_E_INVAL;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  free_all(c);
+  delete c;
+  return RT_OK;
+}
+
+int rt_set_stream(rt_ctx* c, void* s) {
+  if (!c) return RT_E_INVAL;
+  RT_HIP(c, hipStreamSynchronize(c->stream));
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return RT_OK;
+}
+
+void* rt_get_stream(rt_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int rt_synchronize(rt_ctx* c) {
+  if (!c) return RT_E_INVAL;
+  RT_HIP(c, hipStreamSynchronize(c->stream));
+  return RT_OK;
+}
+
+int rt_last_hip_error(rt_ctx* c) { return c ? c->last_hip : 0; }
+
+int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
+  if (!c || !header) return RT_E_INVAL;
+  const int S = c->cfg.num_shapes, spp = c->cfg.spp;
+  if (bytes != rt_header_bytes(S, spp)) return RT_E_INVAL;
+  const float* h = (const float*)header;
+  float mz = h[RT_HDR_MODE * 4 + 2];
+  if (!(mz >= 0.0f && mz < (float)(S + 1))) return RT_E_INVAL;  // int(mode.z) must be in [0, S]
+  int nobj = (int)mz;
+  std::memcpy(c->header.data(), header, bytes);
+  const float* sh = h + rt_off_shapes() / 4;
+  bool allsph = true;
+  for (int i = 0; i < S; ++i) {
+    const float* s = sh + (size_t)i * 20;
+    float idf = s[16 + 3];
+    int id = (idf > -2147483648.0f && idf < 2147483648.0f) ? (int)idf : 0;  // int(simple_shapes[i][4].w)
+    c->table[i] = make_float4(s[0], s[1], s[2], s[3]);
+    float4 g2 = make_float4(s[12], s[13], s[14], 0.0f);
+    std::memcpy(&g2.w, &id, 4);
+    c->table[(size_t)S + i] = g2;
+    c->table[(size_t)2 * S + i] = make_float4(s[16], s[17], s[18], s[19]);
+    c->table[(size_t)3 * S + i] = make_float4(s[4 + 3], s[12 + 3], 0.0f, 0.0f);
+    if (i < nobj && id != RT_SHAPE_SPHERE) allsph = false;
+  }
+  RT_HIP(c, hipSetDevice(c->device));
+  int rc = staged_copy(c, c->d_shapes, c->table.data(), (size_t)4 * std::max(1, S) * sizeof(float4));
+  if (rc != RT_OK) return rc;
+  rc = staged_copy(c, c->d_rb, h + rt_off_rand(S) / 4, (size_t)2 * spp * sizeof(float4));
+  if (rc != RT_OK) return rc;
+  c->nobj = nobj;
+  c->all_spheres = allsph;
+  c->have_header = true;
+  return RT_OK;
+}
+
+int rt_upload_rand_buffer(rt_ctx* c, const float* rb, size_t n_vec4) {
+  if (!c || !rb || n_vec4 != (size_t)2 * c->cfg.spp) return RT_E_INVAL;
+  std::memcpy(c->header.data() + rt_off_rand(c->cfg.num_shapes) / 4, rb, n_vec4 * 16);
+  RT_HIP(c, hipSetDevice(c->device));
+  return staged_copy(c, c->d_rb, rb, n_vec4 * 16);
+}
+
+int rt_run_program(rt_ctx* c, int program, int frame) {
+  if (!c) return RT_E_INVAL;
+  return run_program(c, program, frame);
+}
+
+int rt_dispatch(rt_ctx* c, int mode, int frame) {
+  if (!c) return RT_E_INVAL;
+  int rc;
+  switch (mode) {
+    case RT_MODE_AO_PP:
+      rc = run_program(c, RT_PROG_AOP_COMPUTE, frame);
+      if (rc == RT_OK) rc = run_program(c, RT_PROG_AOP_POSTPROCESSING, frame);
+      break;
+    case RT_MODE_AO: rc = run_program(c, RT_PROG_AO_COMPUTE, frame); break;
+    case RT_MODE_PHONG: rc = run_program(c, RT_PROG_P_COMPUTE, frame); break;
+    case RT_MODE_PHONG_REFL: rc = run_program(c, RT_PROG_H_COMPUTE, frame); break;
+    default: return RT_E_INVAL;
+  }
+  if (rc != RT_OK) return rc;
+  return (frame + 1) % c->cfg.num_frames;
+}
+
+int rt_download(rt_ctx* c, float* pixels, float* normals, float* depth, float* image) {
+  if (!c) return RT_E_INVAL;
+  RT_HIP(c, hipSetDevice(c->device));
+  const int F = c->cfg.num_frames;
+  const size_t slot = slot_elems(c);
+  const size_t ref_slot = (size_t)c->cfg.width * c->own_rows * 4;
+  std::vector<float> tmp(slot * 4);
+  RT_HIP(c, hipStreamSynchronize(c->stream));
+  for (int f = 0; f < F; ++f) {
+    if (pixels) {
+      RT_HIP(c, hipMemcpy(tmp.data(), c->pix[c->pix_slot[f]], slot * 16, hipMemcpyDeviceToHost));
+      dev_to_ref(c, tmp.data(), pixels + f * ref_slot);
+    }
+    if (normals) {
+      RT_HIP(c, hipMemcpy(tmp.data(), c->nrm[f], slot * 16, hipMemcpyDeviceToHost));
+      dev_to_ref(c, tmp.data(), normals + f * ref_slot);
+    }
+    if (depth) {
+      RT_HIP(c, hipMemcpy(tmp.data(), c->dep[f], slot * 16, hipMemcpyDeviceToHost));
+      dev_to_ref(c, tmp.data(), depth + f * ref_slot);
+    }
+  }
+  if (image)
+    RT_HIP(c, hipMemcpy(image, c->d_image, (size_t)c->own_rows * c->cfg.width * 16, hipMemcpyDeviceToHost));
+  return RT_OK;
+}
+
+int rt_upload_gbuffer(rt_ctx* c, const float* pixels, const float* normals, const float* depth) {
+  if (!c) return RT_E_INVAL;
+  RT_HIP(c, hipSetDevice(c->device));
+  const int F = c->cfg.num_frames;
+  const size_t slot = slot_elems(c);
+  const size_t ref_slot = (size_t)c->cfg.width * c->own_rows * 4;
+  std::vector<float> tmp(slot * 4);
+  RT_HIP(c, hipStreamSynchronize(c->stream));
+  for (int f = 0; f < F; ++f) {
+    struct { const float* src; float4* dst; } items[3] = {
+        {pixels, c->pix[c->pix_slot[f]]}, {normals, c->nrm[f]}, {depth, c->dep[f]}};
+    for (auto& it : items) {
+      if (!it.src) continue;
+      RT_HIP(c, hipMemcpy(tmp.data(), it.dst, slot * 16, hipMemcpyDeviceToHost));  // keep halo rows
+      ref_to_dev(c, it.src + f * ref_slot, tmp.data());
+      RT_HIP(c, hipMemcpy(it.dst, tmp.data(), slot * 16, hipMemcpyHostToDevice));
+    }
+  }
+  return RT_OK;
+}
+
+void* rt_image_device_ptr(rt_ctx* c) { return c ? (void*)c->d_image : nullptr; }
+
+int rt_bind_image(rt_ctx* c, void* p) {
+  if (!c) return RT_E_INVAL;
+  c->d_image = p ? (float4*)p : c->d_image_own;
+  return RT_OK;
+}
+
+// ---- host-buffer parity path -----------------------------------------------------------
+static int hostbuf_in(rt_ctx* c, void* ssbo, int frame_num) {
+  if (!c || !ssbo) return RT_E_INVAL;
+  if (c->own0 != 0 || c->own_rows != c->cfg.height) return RT_E_STATE;  // whole-frame contexts only
+  if (frame_num < 0 || frame_num >= c->cfg.num_frames) return RT_E_INVAL;
+  float* f = (float*)ssbo;
+  f[RT_HDR_MODE * 4 + 1] = (float)frame_num;  // ssbo_CPUMEM.mode.y = frame_num (main.cpp:584)
+  const int S = c->cfg.num_shapes, A = c->cfg.spp, W = c->cfg.width, H = c->cfg.height, F = c->cfg.num_frames;
+  int rc = rt_upload_header(c, ssbo, rt_header_bytes(S, A));
+  if (rc != RT_OK) return rc;
+  return rt_upload_gbuffer(c, f + rt_off_pixels(S, A) / 4, f + rt_off_normals(S, A, W, H, F) / 4,
+                           f + rt_off_depth(S, A, W, H, F) / 4);
+}
+
+static int hostbuf_out(rt_ctx* c, void* ssbo, float* image) {
+  float* f = (float*)ssbo;
+  const int S = c->cfg.num_shapes, A = c->cfg.spp, W = c->cfg.width, H = c->cfg.height, F = c->cfg.num_frames;
+  return rt_download(c, f + rt_off_pixels(S, A) / 4, f + rt_off_normals(S, A, W, H, F) / 4,
+                     f + rt_off_depth(S, A, W, H, F) / 4, image);
+}
+
+int rt_compute_one_shader(rt_ctx* c, void* ssbo, int frame_num, int program, float* image) {
+  int rc = hostbuf_in(c, ssbo, frame_num);
+  if (rc != RT_OK) return rc;
+  rc = run_program(c, program, frame_num);
+  if (rc != RT_OK) return rc;
+  rc = hostbuf_out(c, ssbo, image);
+  if (rc != RT_OK) return rc;
+  return (frame_num + 1) % c->cfg.num_frames;
+}
+
+int rt_compute_two_shaders(rt_ctx* c, void* ssbo, int frame_num, int p1, int p2, float* image) {
+  int rc = hostbuf_in(c, ssbo, frame_num);
+  if (rc != RT_OK) return rc;
+  rc = run_program(c, p1, frame_num);
+  if (rc == RT_OK) rc = run_program(c, p2, frame_num);
+  if (rc != RT_OK) return rc;
+  rc = hostbuf_out(c, ssbo, image);
+  if (rc != RT_OK) return rc;
+  return (frame_num + 1) % c->cfg.num_frames;
+}
+
+// ---- instrumentation ------------------------------------------------------------------
+int rt_enable_timing(rt_ctx* c, int on) {
+  if (!c) return RT_E_INVAL;
+  c->timing = on != 0;
+  return RT_OK;
+}
+
+int rt_kernel_stats(rt_ctx* c, int program, int* launches, double* total_ms) {
+  if (!c || program <= 0 || program >= RT_PROG_COUNT) return RT_E_INVAL;
+  int rc = resolve_timing(c);
+  if (rc != RT_OK) return rc;
+  if (launches) *launches = c->launches[program];
+  if (total_ms) *total_ms = c->total_ms[program];
+  return RT_OK;
+}
+
+int rt_reset_stats(rt_ctx* c) {
+  if (!c) return RT_E_INVAL;
+  int rc = resolve_timing(c);
+  if (rc != RT_OK) return rc;
+  for (int k = 0; k < RT_PROG_COUNT; ++k) {
+    c->total_ms[k] = 0.0;
+    c->launches[k] = 0;
+  }
+  return RT_OK;
+}
+
+int rt_selftest_math(rt_ctx* c, int fn, const float* in, float* out, size_t n) {
+  if (!c || !in || !out || fn < 0 || fn > RT_MATH_SPHERE) return RT_E_INVAL;
+  static const int in_w[] = {1, 2, 1, 2, 3, 10}, out_w[] = {1, 1, 1, 1, 3, 1};
+  RT_HIP(c, hipSetDevice(c->device));
+  float *din = nullptr, *dout = nullptr;
+  size_t ib = n * in_w[fn] * sizeof(float), ob = n * out_w[fn] * sizeof(float);
+  RT_HIP(c, hipMalloc(&din, std::max<size_t>(ib, 4)));
+  hipError_t e = hipMalloc(&dout, std::max<size_t>(ob, 4));
+  if (e == hipSuccess) e = hipMemcpy(din, in, ib, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = rt::launch_selftest(fn, din, dout, n, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipMemcpy(out, dout, ob, hipMemcpyDeviceToHost);
+  (void)hipFree(din);
+  if (dout) (void)hipFree(dout);
+  if (e != hipSuccess) return hip_fail(c, e);
+  return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,120 @@
+"""C-ABI library checks that need no GPU: it loads, exports every symbol include/rt/abi.h
+declares, and its host-only helpers (loadShapeBuffer packing, camera basis, rand buffer,
+moving light, scenes) produce the reference's SSBO layout."""
+import ctypes as C
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from real_time_ray_tracer_amd import Header, _lib, aspect_for, header_floats, ssbo_floats
+
+
+def declared_functions():
+    text = (ROOT / "include" / "rt" / "abi.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_every_declared_symbol_is_exported_and_bound():
+    lib = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(lib, n), f"librtrt.so does not export {n}"
+        assert n in _lib.SIGNATURES, f"{n} has no ctypes signature"
+    assert lib.rt_version() == 1
+
+
+def test_layout_matches_reference_instance():
+    # reference ssbo_data: S=10, AA=4, 440x330, F=8 -> 1,040 B header, 55,757,840 B total
+    assert header_floats(10, 4) * 4 == 1040
+    assert ssbo_floats(10, 4, 440, 330, 8) * 4 == 55_757_840
+
+
+def test_pack_sphere_plane_rectangle_layout():
+    h = Header(10, 4)
+    h.pack_sphere(0, (1, 2, 3), 4.0, (0.1, 0.2, 0.3), reflectivity=0.5, emissive=True)
+    s = h.shapes[0]
+    np.testing.assert_array_equal(s[0], [1, 2, 3, 4])
+    assert s[1, 3] == 1.0 and s[3, 3] == 0.5
+    np.testing.assert_array_equal(s[4], np.float32([0.1, 0.2, 0.3, 1]))
+    h.pack_plane(1, (0, 2, 0), -4.0, (0.3, 0.0, 0.5))
+    p = h.shapes[1]
+    np.testing.assert_array_equal(p[0], [0, 1, 0, -4])          # normalize(normal), dist
+    np.testing.assert_array_equal(p[3], [0, -8, 0, 1])          # p0 = dist * (unnormalised) normal
+    assert p[4, 3] == 5.0
+    h.pack_rectangle(2, (4, 6, 4), (0, 0, -8), (-8, 0, 0), (1.5, 1.5, 1.5), emissive=True)
+    r = h.shapes[2]
+    assert r[4, 3] == 3.0 and r[1, 3] == 1.0
+    np.testing.assert_allclose(r[0, :3], [0, 1, 0], atol=1e-7)  # normalize(cross(right, up))
+    with pytest.raises(_lib.RtError):
+        h.pack_sphere(10, (0, 0, 0), 1, (1, 1, 1))
+
+
+def test_camera_basis_default_pose():
+    h = Header(1, 1)
+    h.camera_basis((0, 0, 14), (0, 1, 0), (0, 0, 1), 1.333333)
+    np.testing.assert_array_equal(h.vec4(1), np.float32([1.333333, 0, 0, 0]))
+    np.testing.assert_array_equal(h.vec4(2), [0, 1, 0, 0])
+    np.testing.assert_allclose(h.vec4(3), [-0.6666665, -0.5, -1, 0], rtol=1e-7)
+    np.testing.assert_array_equal(h.vec4(4), [0, 0, 14, 0])
+
+
+def test_rand_buffer_seeded_and_in_unit_interval():
+    a, b = Header(4, 16), Header(4, 16)
+    a.fill_rand_buffer(7000)
+    b.fill_rand_buffer(7000)
+    np.testing.assert_array_equal(a.rand_buffer, b.rand_buffer)
+    assert a.rand_buffer.shape == (32, 4)
+    assert (a.rand_buffer >= 0).all() and (a.rand_buffer < 1).all()
+    b.fill_rand_buffer(7001)
+    assert not np.array_equal(a.rand_buffer, b.rand_buffer)
+
+
+def test_moving_light():
+    h = Header(1, 1)
+    h.moving_light(False)
+    np.testing.assert_array_equal(h.vec4(5), [-12, 8, 7, 0])
+    h.moving_light(True)
+    np.testing.assert_array_equal(h.vec4(5), np.float32([-12, 8, 7, 0]) + np.float32(0.1))
+    h.data[20] = 50.05
+    h.moving_light(True)
+    np.testing.assert_array_equal(h.vec4(5), [-50, 20, -50, 0])
+
+
+def test_synthetic_scene_matches_survey_recipe():
+    h = Header.synthetic(64, 16, 1234 + 3, aspect_for(3840, 2160))
+    assert h.num_objects == 64
+    s = h.shapes
+    np.testing.assert_array_equal(s[0, 0], [0, -35, 0, 33])
+    c = s[1:, 0]
+    assert (c[:, 0] >= -12).all() and (c[:, 0] <= 12).all()
+    assert (c[:, 1] >= -2).all() and (c[:, 1] <= 6).all()
+    assert (c[:, 2] >= -20).all() and (c[:, 2] <= 4).all()
+    assert (c[:, 3] >= 0.3).all() and (c[:, 3] <= 1.5).all()
+    assert (s[:, 4, 3] == 1).all()
+    refl = s[1:, 3, 3]
+    assert ((refl == 1.0) | (refl <= 0.6)).all()
+    np.testing.assert_array_equal(h.vec4(6), np.float32([13 / 255.0, 153 / 255.0, 219 / 255.0, 0]))
+    h2 = Header.synthetic(64, 16, 1234 + 3, aspect_for(3840, 2160))
+    np.testing.assert_array_equal(h.data, h2.data)
+
+
+def test_builtin_scenes():
+    for which, n in ((1, 5), (5, 3), (6, 6)):
+        h = Header.builtin(which, 4)
+        assert h.num_objects == n
+    h1 = Header.builtin(1, 4)
+    assert h1.shapes[4, 4, 3] == 5.0  # scene1's plane
+
+
+def test_create_without_gpu_reports_nodev(gpu_available):
+    if gpu_available:
+        pytest.skip("a GPU is present")
+    lib = _lib.load()
+    cfg = _lib.rt_config(64, 48, 10, 4, 8, 20, 0, 0)
+    ctx = C.c_void_p()
+    assert lib.rt_create(0, C.byref(cfg), C.byref(ctx)) == _lib.RT_E_NODEV
+    assert lib.rt_strerror(_lib.RT_E_NODEV) == b"no HIP device"
