@@ -1,0 +1,265 @@
+#!/usr/bin/env python
+"""Benchmark: Mrays/s + ms/frame of the per-pixel ray-scene hot path (BASELINE.json metric).
+
+Workload (default, BASELINE.json configs[3] = SURVEY §8d config (d)): 3840x2160, 64 spheres,
+AO 16 spp + temporal/spatial post-process (mode 1 = aop_compute + aop_postprocessing),
+synthetic seeded scene (scene seed 1234+3, per-frame rand_buffer seed 7000+k).
+
+One step = one frame: host header update (fill_rand_buffer, mode.y) -> upload -> AO pass ->
+post-process pass (-> on N>1, gather of the image strips into rank 0 over RCCL, pipelined).
+N GPUs split the SAME frame into cost-balanced row strips (strong scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config b|c|d|e]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  Mrays/s = W*H*spp*K / time (primary samples, whole job).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+CONFIGS = {
+    # name: (W, H, spheres, spp, mode, description)
+    "a": (640, 480, 4, 1, 3, "config (a): 640x480, 4 spheres, Phong (mode 3), 1 spp"),
+    "b": (1920, 1080, 16, 1, 4, "config (b): 1920x1080, 16 spheres, Phong + reflections (mode 4, <=20 bounces), 1 spp"),
+    "c": (1920, 1080, 64, 16, 2, "config (c): 1920x1080, 64 spheres, AO 16 spp (mode 2)"),
+    "d": (3840, 2160, 64, 16, 1, "config (d): 3840x2160, 64 spheres, AO 16 spp + temporal/spatial post-process (mode 1)"),
+    "e": (7680, 4320, 256, 64, 2, "config (e): 7680x4320, 256 spheres, AO 64 spp (mode 2)"),
+}
+CONFIG_INDEX = {"a": 0, "b": 1, "c": 2, "d": 3, "e": 4}
+
+FLOP_PER_TEST = 20          # ~20 FLOP per ray-sphere test (FMA = 2 FLOP)
+PEAK_FP32_TFLOPS = 157.3    # MI355X_MICROARCH.md: peak FP32 vector (spec)
+PEAK_HBM_GBPS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
+# algorithmic HBM bytes per pixel per launch: mode-1 pass 1 writes raw colour +
+# normal + depth (48 B); pass 2 unique minimum reads 48 B + writes pixel + image (32 B)
+BYTES_PER_PIXEL = {1: 48, 2: 80, 3: 64, 4: 32, 5: 32}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(cfg_name: str, target_s: float) -> dict:
+    """The CPU oracle (oracle/rt_oracle.c, OpenMP over rows) on a bounded, evenly spread sample
+    of rows of the same frame; both mode-1 passes for config (d)."""
+    import oracle
+    from real_time_ray_tracer_amd import Header, aspect_for
+
+    W, H, S, spp, mode, _ = CONFIGS[cfg_name]
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    h = Header.synthetic(S, spp, 1234 + CONFIG_INDEX[cfg_name], aspect_for(W, H))
+    progs = {1: [oracle.AOP_COMPUTE, oracle.AOP_POSTPROCESSING], 2: [oracle.AO_COMPUTE],
+             3: [oracle.P_COMPUTE], 4: [oracle.H_COMPUTE]}[mode]
+
+    def run_rows(rows):
+        t = 0.0
+        for y in rows:
+            d = oracle.dims(W, H, S, spp, gy0=int(y), gh=1)
+            buf = np.zeros(h.data.size + 3 * 8 * W * 4, np.float32)
+            buf[:h.data.size] = h.data
+            t0 = time.perf_counter()
+            for p in progs:
+                oracle.run_program(buf, d, p, 0, None, nthreads=threads)
+            t += time.perf_counter() - t0
+        return t
+
+    probe = run_rows([H // 2])
+    n = int(max(2, min(H, target_s / max(probe, 1e-4))))
+    rows = [int((i + 0.5) * H / n) for i in range(n)]
+    t = run_rows(rows)
+    units = len(rows) * W * (spp if mode in (1, 2) else 1)
+    return {"value": round(units / t / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{len(rows)} of {H} rows (evenly spread) x {W} px x {spp if mode in (1, 2) else 1} spp, "
+                      f"{'+'.join({1: 'aop_compute', 2: 'aop_postprocessing', 3: 'ao_compute', 4: 'p_compute', 5: 'h_compute'}[p] for p in progs)}, "
+                      f"oracle/rt_oracle.c with {threads} OpenMP threads, {t:.1f} s; ms/frame extrapolated "
+                      f"{t / len(rows) * H * 1e3:.0f}"}
+
+
+def load_traffic(cfg_name: str):
+    """HBM bytes per launch measured with rocprofv3 PMC passes (profiles/*_pmc.json)."""
+    for p in sorted(ROOT.glob("profiles/*_pmc.json"), reverse=True):
+        try:
+            data = json.loads(p.read_text())
+        except Exception:
+            continue
+        if data.get("config") == cfg_name:
+            return data, p.name
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--config", default="d", choices=sorted(CONFIGS))
+    ap.add_argument("--no-balance", action="store_true", help="equal strips instead of cost-balanced")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    from real_time_ray_tracer_amd import Header, Renderer, aspect_for
+    from real_time_ray_tracer_amd.dist import StripGather, StripPlan, balanced_bounds, equal_bounds
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    W, H, S, spp, mode, desc = CONFIGS[args.config]
+    header = Header.synthetic(S, spp, 1234 + CONFIG_INDEX[args.config], aspect_for(W, H))
+    stream = torch.cuda.current_stream(dev)
+
+    # ---- strip plan: cost-balanced from the kernels' per-row segment counts -----------------
+    bounds = equal_bounds(H, world)
+    if world > 1 and not args.no_balance:
+        probe = Renderer(W, H, S, spp, device=local_rank, rows=(bounds[rank], bounds[rank + 1]))
+        probe.set_stream(stream.cuda_stream)
+        probe.enable_counters(True)
+        header.fill_rand_buffer(7000)
+        header.set_mode(0, S)
+        probe.upload_header(header)
+        probe.dispatch(mode, 0)
+        mine = probe.read_row_counters().astype(np.float64)
+        probe.close()
+        full = torch.zeros(H, dtype=torch.float64, device=dev)
+        full[bounds[rank]:bounds[rank + 1]] = torch.from_numpy(mine).to(dev)
+        dist.all_reduce(full)
+        bounds = balanced_bounds(full.cpu().numpy(), world)
+    plan = StripPlan(W, H, bounds)
+    r0, r1 = plan.rows(rank)
+    rend = Renderer(W, H, S, spp, device=local_rank, rows=(r0, r1))
+    rend.set_stream(stream.cuda_stream)
+    gather = StripGather(plan, rank, dev) if world > 1 else None
+    state = {"frame": 0}
+
+    def step(k: int):
+        if mode in (1, 2):
+            header.fill_rand_buffer(7000 + k)
+        else:
+            header.moving_light(False)
+        header.set_mode(state["frame"], S)
+        rend.upload_header(header)
+        if gather is not None:
+            rend.bind_image(gather.strip(k).data_ptr())
+        state["frame"] = rend.dispatch(mode, state["frame"])
+        if gather is not None:
+            gather.gather(k)
+
+    for k in range(args.warmup):
+        step(k)
+    if gather is not None:
+        gather.finish()
+    torch.cuda.synchronize()
+
+    # ---- timed region -----------------------------------------------------------------------
+    rend.enable_timing(True)
+    rend.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.warmup, args.warmup + args.steps):
+        step(k)
+    if gather is not None:
+        gather.finish()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    rend.enable_timing(False)
+    progs = {1: [1, 2], 2: [3], 3: [4], 4: [5]}[mode]
+    kstats = {p: rend.kernel_stats(p) for p in progs}
+
+    # ---- work counters (un-timed re-run of two timed frames' inputs) ------------------------
+    rend.enable_counters(True)
+    rend.read_counters(reset=True)
+    ncount = 2
+    for k in range(args.warmup, args.warmup + ncount):
+        step(k)
+    if gather is not None:
+        gather.finish()
+    counts = rend.read_counters(reset=True)
+    rend.enable_counters(False)
+
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    elapsed = float(t_max.item())
+
+    if rank == 0:
+        rays_per_frame = W * H * (spp if mode in (1, 2) else 1)
+        value = rays_per_frame * args.steps / elapsed / 1e6
+        ms = elapsed / args.steps * 1e3
+        dom = progs[0]
+        n_l, tot = kstats[dom]
+        avg_ms = tot / max(n_l, 1)
+        tests = counts["tests"] / ncount
+        tflops = FLOP_PER_TEST * tests / (avg_ms * 1e-3) / 1e12
+        band_px = (r1 - r0 + (2 if mode in (1, 2) and world > 1 else 0)) * W
+        hbm_alg = BYTES_PER_PIXEL[dom] * band_px / (avg_ms * 1e-3) / 1e9
+        traffic_data, traffic_src = load_traffic(args.config)
+        roof = {
+            "bound": "valu",
+            "achieved": round(tflops, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tflops / PEAK_FP32_TFLOPS, 4),
+            "traffic": traffic_data.get(str(dom)) if traffic_data else None,
+            "kernel": {1: "aop_compute (ao_kernel)", 3: "ao_compute (ao_kernel)", 4: "p_compute (phong_kernel)",
+                       5: "h_compute (hybrid_kernel)"}[dom],
+            "kernel_ms": round(avg_ms, 4),
+            "flop_per_launch": FLOP_PER_TEST * tests,
+            "tests_per_launch": tests,
+            "segments_per_sample": round(counts["segments"] / max(counts["samples"], 1), 4),
+            "hbm": {"achieved": round(hbm_alg, 2), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                    "frac": round(hbm_alg / PEAK_HBM_GBPS, 6),
+                    "bytes_per_launch": BYTES_PER_PIXEL[dom] * band_px},
+            "traffic_source": traffic_src,
+        }
+        out = {
+            "metric": "Mrays/s + ms/frame at 3840x2160, 16 AO samples, 64 spheres; 1/2/4/8 GPU",
+            "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": desc, "width": W, "height": H, "spheres": S, "spp": spp, "mode": mode,
+                       "max_depth": 20, "strips": plan.bounds,
+                       "parallelism": f"{world} row strip(s), cost-balanced" + (", RCCL gather to rank 0" if world > 1 else "")},
+            "roofline": roof,
+        }
+        if mode == 1:
+            n_p, tot_p = kstats[2]
+            pms = tot_p / max(n_p, 1)
+            pbw = BYTES_PER_PIXEL[2] * (r1 - r0) * W / (pms * 1e-3) / 1e9
+            out["roofline_post"] = {"bound": "hbm", "achieved": round(pbw, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                                    "frac": round(pbw / PEAK_HBM_GBPS, 4), "kernel": "aop_postprocessing (post_kernel)",
+                                    "kernel_ms": round(pms, 4),
+                                    "traffic": traffic_data.get("2") if traffic_data else None}
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
+            except Exception as e:  # the checker must not take the GPU number down with it
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(out), flush=True)
+    rend.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

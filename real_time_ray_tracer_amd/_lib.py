@@ -57,6 +57,9 @@ SIGNATURES = {
     "rt_enable_timing": (C.c_int, [_ctx, C.c_int]),
     "rt_kernel_stats": (C.c_int, [_ctx, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]),
     "rt_reset_stats": (C.c_int, [_ctx]),
+    "rt_enable_counters": (C.c_int, [_ctx, C.c_int]),
+    "rt_read_counters": (C.c_int, [_ctx, C.POINTER(C.c_uint64), C.c_int]),
+    "rt_read_row_counters": (C.c_int, [_ctx, C.POINTER(C.c_uint64), C.c_int]),
     "rt_selftest_math": (C.c_int, [_ctx, C.c_int, _fp, _fp, C.c_size_t]),
     "rt_pack_sphere": (C.c_int, [_fp, C.c_int, C.c_int, _fp, C.c_float, _fp, C.c_float, C.c_int]),
     "rt_pack_plane": (C.c_int, [_fp, C.c_int, C.c_int, _fp, C.c_float, _fp, C.c_float, C.c_int]),

@@ -32,6 +32,11 @@ struct FrameParams {
   const float4* hist_pix[kMaxFrames];  // per slot
   const float4* hist_nrm[kMaxFrames];
   const float4* hist_dep[kMaxFrames];
+  // optional work counters (nullptr in timed runs): [0] primary samples, [1] closest-hit
+  // segments, [2] shadow rays, [3] ray-shape tests = (segments + shadow rays) * nobj
+  unsigned long long* counters;
+  // optional per-row closest-hit segment counts, indexed by (y - band_row0) (nullptr = off)
+  unsigned long long* row_counters;
 };
 
 enum KernelId { K_AOP = 1, K_POST = 2, K_AO = 3, K_PHONG = 4, K_HYBRID = 5 };

@@ -49,6 +49,18 @@ __device__ __forceinline__ void tile_xy(int& x, int& y, int row0) {
   y = row0 + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
 }
 
+// Work counters for the algorithmic-FLOP roofline (only when P.counters is set; the atomic
+// optimizer turns the uniform-address adds into one add per wave).
+__device__ __forceinline__ void count_work(const FrameParams& P, int y, unsigned samples, unsigned segs,
+                                           unsigned shadows) {
+  if (P.row_counters) atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)(segs + shadows));
+  if (!P.counters) return;
+  atomicAdd(&P.counters[0], (unsigned long long)samples);
+  atomicAdd(&P.counters[1], (unsigned long long)segs);
+  atomicAdd(&P.counters[2], (unsigned long long)shadows);
+  atomicAdd(&P.counters[3], (unsigned long long)(segs + shadows) * (unsigned long long)P.nobj);
+}
+
 __device__ __forceinline__ void store_color(const FrameParams& P, int x, int y, float4 c) {
   P.out_pix[(size_t)(y - P.band_row0) * P.W + x] = c;
   if (P.image) {
@@ -75,6 +87,7 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
   f3 dir = primary_dir(P, (float)x / (float)P.W, (float)y / (float)P.H);
   float t;
   int ind = closest_hit<ALLSPH>(geo, geo2, n, cam, dir, 0.0f, t);
+  count_work(P, y, 1u, 1u, ind == -1 ? 0u : 1u);
   float r, g, b;
   if (ind == -1) {
     r = P.bg.x; g = P.bg.y; b = P.bg.z;
@@ -117,10 +130,13 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
   float arefl = 0.0f;          // array[2].w
   float rr = 0, rg = 0, rb = 0;  // result_color.rgb
   float c = 0.0f;
+  unsigned nseg = 0, nshadow = 0;
   for (int seg = 0; seg < P.D; ++seg) {  // helper depth D, D-1, ..., 1
     // ---- hybrid_helper ----
     float t;
     int ind = closest_hit<ALLSPH>(geo, geo2, n, pos, dir, 0.001f, t);
+    ++nseg;
+    nshadow += ind == -1 ? 0u : 1u;
     float ar, ag, ab;
     bool stop;
     if (ind == -1) {
@@ -165,6 +181,7 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
     }
     if (stop) break;
   }
+  count_work(P, y, 1u, nseg, nshadow);
   store_color(P, x, y, gamma_out(0.0f + rr, 0.0f + rg, 0.0f + rb));
 }
 
@@ -225,9 +242,11 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P) {
     }
     const f3 cam = mk(P.cx, P.cy, P.cz);
     f3 pos = cam;
+    unsigned nseg = 0;
     for (int depth = P.D; depth > 0; --depth) {
       float t;
       int ind = closest_hit<ALLSPH>(geo, geo2, n, pos, dir, 0.0001f, t);
+      ++nseg;
       if (ind != -1) {
         float4 att = col[ind];
         float4 ax = aux[ind];
@@ -263,6 +282,7 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P) {
         break;
       }
     }
+    count_work(P, y, 1u, nseg, 0u);
   }
   samp[threadIdx.x] = make_float4(rr, rg, rb, stopv);
   __syncthreads();

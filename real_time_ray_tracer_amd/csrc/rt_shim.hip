@@ -65,6 +65,9 @@ struct rt_ctx {
   std::vector<hipEvent_t> event_pool;
   double total_ms[RT_PROG_COUNT] = {};
   int launches[RT_PROG_COUNT] = {};
+  unsigned long long* d_counters = nullptr;
+  unsigned long long* d_row_counters = nullptr;  // [band_rows]
+  bool counting = false;
   int last_hip = 0;
 };
 
@@ -132,6 +135,8 @@ void free_all(rt_ctx* c) {
   if (c->d_image_own) (void)hipFree(c->d_image_own);
   if (c->d_shapes) (void)hipFree(c->d_shapes);
   if (c->d_rb) (void)hipFree(c->d_rb);
+  if (c->d_counters) (void)hipFree(c->d_counters);
+  if (c->d_row_counters) (void)hipFree(c->d_row_counters);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
 }
 
@@ -170,6 +175,8 @@ void fill_params(const rt_ctx* c, int frame, rt::FrameParams& p) {
   }
   p.nrm = c->nrm[frame];
   p.dep = c->dep[frame];
+  p.counters = c->counting ? c->d_counters : nullptr;
+  p.row_counters = c->counting ? c->d_row_counters : nullptr;
 }
 
 int launch(rt_ctx* c, int program, const rt::FrameParams& p) {
@@ -554,6 +561,50 @@ int rt_reset_stats(rt_ctx* c) {
     c->total_ms[k] = 0.0;
     c->launches[k] = 0;
   }
+  return RT_OK;
+}
+
+int rt_enable_counters(rt_ctx* c, int on) {
+  if (!c) return RT_E_INVAL;
+  RT_HIP(c, hipSetDevice(c->device));
+  if (on && !c->d_counters) {
+    RT_HIP(c, hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long)));
+    RT_HIP(c, hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
+    RT_HIP(c, hipMalloc(&c->d_row_counters, (size_t)c->band_rows * sizeof(unsigned long long)));
+    RT_HIP(c, hipMemsetAsync(c->d_row_counters, 0, (size_t)c->band_rows * sizeof(unsigned long long), c->stream));
+  }
+  c->counting = on != 0;
+  return RT_OK;
+}
+
+int rt_read_counters(rt_ctx* c, uint64_t out[4], int reset) {
+  if (!c || !out) return RT_E_INVAL;
+  if (!c->d_counters) {
+    for (int k = 0; k < 4; ++k) out[k] = 0;
+    return RT_OK;
+  }
+  RT_HIP(c, hipSetDevice(c->device));
+  unsigned long long h[4];
+  RT_HIP(c, hipStreamSynchronize(c->stream));
+  RT_HIP(c, hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
+  for (int k = 0; k < 4; ++k) out[k] = (uint64_t)h[k];
+  if (reset) RT_HIP(c, hipMemset(c->d_counters, 0, sizeof(h)));
+  return RT_OK;
+}
+
+int rt_read_row_counters(rt_ctx* c, uint64_t* rows, int reset) {
+  if (!c || !rows) return RT_E_INVAL;
+  const int R = c->own_rows;
+  if (!c->d_row_counters) {
+    for (int k = 0; k < R; ++k) rows[k] = 0;
+    return RT_OK;
+  }
+  RT_HIP(c, hipSetDevice(c->device));
+  std::vector<unsigned long long> h(c->band_rows);
+  RT_HIP(c, hipStreamSynchronize(c->stream));
+  RT_HIP(c, hipMemcpy(h.data(), c->d_row_counters, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  for (int k = 0; k < R; ++k) rows[k] = (uint64_t)h[(size_t)(c->own0 - c->band0) + k];
+  if (reset) RT_HIP(c, hipMemset(c->d_row_counters, 0, h.size() * sizeof(unsigned long long)));
   return RT_OK;
 }
 

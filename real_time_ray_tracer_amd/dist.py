@@ -1,0 +1,122 @@
+"""Multi-GPU row strips + gather of the image strips to rank 0.
+
+SURVEY.md §8e: every trace pixel is independent, so a frame is cut into N contiguous row
+strips, one per GPU (one process per GPU, torch.distributed over RCCL/xGMI).  Each rank
+keeps its own g-buffer ring for its strip plus a 1-row halo (rendered redundantly, so the
+post-process needs no exchange); the only collective is the per-frame gather of the final
+image strips into rank 0.  Strip bounds are balanced by a per-row cost profile (segment
+counts from the kernels' row counters), because sky rows are far cheaper than ground rows.
+
+The gather is pipelined: frame k's strip is gathered (async, RCCL stream) while frame k+1
+renders into the other of two image buffers.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+
+def equal_bounds(H: int, n: int) -> list[int]:
+    return [round(i * H / n) for i in range(n + 1)]
+
+
+def balanced_bounds(row_cost: np.ndarray, n: int, min_rows: int = 1) -> list[int]:
+    """Contiguous strips of (nearly) equal total cost.  row_cost[y] >= 0 for every frame row."""
+    H = len(row_cost)
+    c = np.asarray(row_cost, np.float64) + 1e-9 * max(1.0, float(np.max(row_cost)) if H else 1.0)
+    cum = np.concatenate([[0.0], np.cumsum(c)])
+    total = cum[-1]
+    b = [0]
+    for i in range(1, n):
+        y = int(np.searchsorted(cum, total * i / n))
+        y = max(y, b[-1] + min_rows)
+        y = min(y, H - (n - i) * min_rows)
+        b.append(y)
+    b.append(H)
+    return b
+
+
+def strip_cost(bounds: list[int], row_cost: np.ndarray) -> list[float]:
+    return [float(np.sum(row_cost[bounds[i]:bounds[i + 1]])) for i in range(len(bounds) - 1)]
+
+
+@dataclass
+class StripPlan:
+    W: int
+    H: int
+    bounds: list[int]
+
+    @property
+    def n(self) -> int:
+        return len(self.bounds) - 1
+
+    def rows(self, rank: int) -> tuple[int, int]:
+        return self.bounds[rank], self.bounds[rank + 1]
+
+    @property
+    def max_rows(self) -> int:
+        return max(self.bounds[i + 1] - self.bounds[i] for i in range(self.n))
+
+    def assemble(self, padded_strips: list) -> "np.ndarray | object":
+        """Concatenate the gathered (padded) strips into the [H][W][4] frame."""
+        parts = [padded_strips[i][: self.bounds[i + 1] - self.bounds[i]] for i in range(self.n)]
+        if isinstance(parts[0], np.ndarray):
+            return np.concatenate(parts, 0)
+        import torch
+
+        return torch.cat(parts, 0)
+
+
+class StripGather:
+    """Gathers every rank's [max_rows][W][4] image strip into rank 0 with torch.distributed
+    (RCCL on GPUs, gloo on CPU).  Strips are padded to max_rows so one gather moves them all;
+    with equal strips the gather lands directly in the frame tensor (no assembly copy)."""
+
+    def __init__(self, plan: StripPlan, rank: int, device, nbuf: int = 2, root: int = 0):
+        import torch
+
+        self.plan, self.rank, self.root, self.nbuf = plan, rank, root, nbuf
+        R, W = plan.max_rows, plan.W
+        self.equal = all(plan.bounds[i + 1] - plan.bounds[i] == R for i in range(plan.n))
+        self.strips = [torch.zeros((R, W, 4), dtype=torch.float32, device=device) for _ in range(nbuf)]
+        self.frames = []
+        self.lists = []
+        if rank == root:
+            for _ in range(nbuf):
+                frame = torch.zeros((plan.n * R, W, 4), dtype=torch.float32, device=device)
+                self.frames.append(frame)
+                self.lists.append(list(frame.split(R, 0)))
+        self.pending = [None] * nbuf
+
+    def strip(self, k: int):
+        """Image buffer frame k renders into (waits for the gather that last used it)."""
+        i = k % self.nbuf
+        if self.pending[i] is not None:
+            self.pending[i].wait()
+            self.pending[i] = None
+        return self.strips[i]
+
+    def gather(self, k: int, async_op: bool = True):
+        import torch.distributed as dist
+
+        i = k % self.nbuf
+        lst = self.lists[i] if self.rank == self.root else None
+        work = dist.gather(self.strips[i], gather_list=lst, dst=self.root, async_op=async_op)
+        if async_op:
+            self.pending[i] = work
+
+    def finish(self):
+        for i, w in enumerate(self.pending):
+            if w is not None:
+                w.wait()
+                self.pending[i] = None
+
+    def frame(self, k: int):
+        """Rank 0: the assembled [H][W][4] frame of frame k (after finish())."""
+        if self.rank != self.root:
+            return None
+        full = self.frames[k % self.nbuf]
+        if self.equal:
+            return full
+        return self.plan.assemble(self.lists[k % self.nbuf])

@@ -272,6 +272,20 @@ class Renderer:
     def reset_stats(self):
         self._c(self._lib.rt_reset_stats(self.ctx), "rt_reset_stats")
 
+    def enable_counters(self, on: bool = True):
+        self._c(self._lib.rt_enable_counters(self.ctx, int(on)), "rt_enable_counters")
+
+    def read_counters(self, reset: bool = True) -> dict:
+        out = (C.c_uint64 * 4)()
+        self._c(self._lib.rt_read_counters(self.ctx, out, int(reset)), "rt_read_counters")
+        return {"samples": out[0], "segments": out[1], "shadow_rays": out[2], "tests": out[3]}
+
+    def read_row_counters(self, reset: bool = True) -> np.ndarray:
+        out = np.zeros(self.R, np.uint64)
+        self._c(self._lib.rt_read_row_counters(self.ctx, out.ctypes.data_as(C.POINTER(C.c_uint64)), int(reset)),
+                "rt_read_row_counters")
+        return out
+
     def selftest_math(self, fn: int, inputs: np.ndarray, n: int) -> np.ndarray:
         out_w = {_lib.RT_MATH_NORMALIZE: 3}.get(fn, 1)
         inp = np.ascontiguousarray(inputs, np.float32).reshape(-1)

@@ -1,0 +1,109 @@
+"""Multi-rank strip path on CPU (gloo, world_size 2 and 3): cost-balanced row strips, each
+rendered with its 1-row halo band (the oracle plays the GPU here), gathered into rank 0 by
+real.dist.StripGather, must equal the whole-frame render bit for bit over a multi-frame
+mode-1 sequence (temporal history + spatial neighbours across strip edges)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT  # noqa: F401  (sys.path)
+
+W, H, FRAMES = 40, 30, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _header():
+    from real_time_ray_tracer_amd import Header, aspect_for
+
+    return Header.synthetic(12, 4, 99, aspect_for(W, H))
+
+
+def _render_band(h, gy0, gh, own0, own1, frames):
+    """Oracle render of a band (strip + halo) over a frame sequence; returns own-row images."""
+    import oracle
+
+    d = oracle.dims(W, H, h.S, h.AA, gy0=gy0, gh=gh)
+    buf = np.zeros(h.data.size + 3 * 8 * W * gh * 4, np.float32)
+    imgs = []
+    f = 0
+    for k in range(frames):
+        hk = h.copy()
+        hk.fill_rand_buffer(7000 + k)
+        hk.set_mode(f, hk.num_objects)
+        buf[:hk.data.size] = hk.data
+        img = np.zeros((gh, W, 4), np.float32)
+        oracle.run_program(buf, d, oracle.AOP_COMPUTE, f, None, gy0, gy0 + gh, nthreads=1)
+        oracle.run_program(buf, d, oracle.AOP_POSTPROCESSING, f, img, own0, own1, nthreads=1)
+        imgs.append(img[own0 - gy0:own1 - gy0].copy())
+        f = (f + 1) % 8
+    return imgs
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from real_time_ray_tracer_amd.dist import StripGather, StripPlan, balanced_bounds
+
+        cost = np.linspace(1.0, 5.0, H) ** 2  # ground rows dearer than sky rows
+        plan = StripPlan(W, H, balanced_bounds(cost, world))
+        r0, r1 = plan.rows(rank)
+        b0, b1 = max(0, r0 - 1), min(H, r1 + 1)
+        imgs = _render_band(_header(), b0, b1 - b0, r0, r1, FRAMES)
+        g = StripGather(plan, rank, "cpu")
+        for k in range(FRAMES):
+            s = g.strip(k)
+            s.zero_()
+            s[: r1 - r0] = torch.from_numpy(imgs[k])
+            g.gather(k)
+        g.finish()
+        if rank == 0:
+            q.put(("ok", plan.bounds, g.frame(FRAMES - 1).numpy().copy()))
+    except Exception as e:  # pragma: no cover - reported through the queue
+        q.put(("err", repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_strips_gathered_equal_whole_frame(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    status, bounds, frame = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    assert status == "ok", bounds
+    assert len(bounds) == world + 1 and bounds[0] == 0 and bounds[-1] == H
+    full = _render_band(_header(), 0, H, 0, H, FRAMES)[-1]
+    assert frame.shape == full.shape
+    assert np.array_equal(frame.view(np.uint32), full.view(np.uint32))
+
+
+def test_balanced_bounds_equalise_cost():
+    from real_time_ray_tracer_amd.dist import balanced_bounds, equal_bounds, strip_cost
+
+    cost = np.r_[np.full(1000, 1.0), np.full(1160, 9.0)]  # cheap sky, dear ground
+    b = balanced_bounds(cost, 8)
+    c = strip_cost(b, cost)
+    assert max(c) / min(c) < 1.02
+    eq = strip_cost(equal_bounds(2160, 8), cost)
+    assert max(eq) / np.mean(eq) > 1.5 > max(c) / np.mean(c)
+    assert balanced_bounds(np.zeros(10), 3) == [0, 3, 7, 10] or len(balanced_bounds(np.zeros(10), 3)) == 4
