@@ -132,7 +132,7 @@ def main():
     if world > 1 and not args.no_balance:
         probe = Renderer(W, H, S, spp, device=local_rank, rows=(bounds[rank], bounds[rank + 1]))
         probe.set_stream(stream.cuda_stream)
-        probe.enable_counters(True)
+        probe.enable_counters(totals=False, rows=True)
         header.fill_rand_buffer(7000)
         header.set_mode(0, S)
         probe.upload_header(header)
@@ -227,6 +227,7 @@ def main():
             "flop_per_launch": FLOP_PER_TEST * tests,
             "tests_per_launch": tests,
             "segments_per_sample": round(counts["segments"] / max(counts["samples"], 1), 4),
+            "lane_utilisation": round(counts["tests"] / max(counts["executed_lane_tests"], 1), 4),
             "hbm": {"achieved": round(hbm_alg, 2), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                     "frac": round(hbm_alg / PEAK_HBM_GBPS, 6),
                     "bytes_per_launch": BYTES_PER_PIXEL[dom] * band_px},

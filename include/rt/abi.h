@@ -126,13 +126,15 @@ int rt_enable_timing(rt_ctx* ctx, int on);
 /* Sum of event-measured durations of `program`'s kernel since the last reset. */
 int rt_kernel_stats(rt_ctx* ctx, int program, int* launches, double* total_ms);
 int rt_reset_stats(rt_ctx* ctx);
-/* Work counters (a separate, un-timed instrumentation mode): when on, every trace launch adds
- * [0] primary samples, [1] closest-hit segments (one scene loop each), [2] shadow rays,
- * [3] ray-shape tests = ([1] + [2]) * int(mode.z) — the algorithmic-FLOP basis of the
- * roofline (20 FLOP per ray-sphere test). */
+/* Work counters (a separate, un-timed instrumentation mode).  on = bit 0: totals, bit 1:
+ * per-row counts.  Totals, added by every trace launch: [0] primary samples, [1] closest-hit
+ * segments (one scene loop each), [2] shadow rays, [3] ray-shape tests = ([1] + [2]) *
+ * int(mode.z) — the algorithmic-FLOP basis of the roofline (20 FLOP per ray-sphere test,
+ * SURVEY.md §8d), [4] executed lane-tests = sum over wavefronts of 64 x the shapes their scene
+ * loops tested (divergence and culling: [3]/[4] is the useful fraction). */
 int rt_enable_counters(rt_ctx* ctx, int on);
-/* Read the 4 counters (synchronises); reset != 0 zeroes them afterwards. */
-int rt_read_counters(rt_ctx* ctx, uint64_t out[4], int reset);
+/* Read the 5 totals (synchronises); reset != 0 zeroes them afterwards. */
+int rt_read_counters(rt_ctx* ctx, uint64_t out[5], int reset);
 /* Per-row segment + shadow-ray counts of this context's rows (R = row_end - row_begin
  * entries), collected while counters are on: the cost profile used to balance row strips
  * across GPUs. */

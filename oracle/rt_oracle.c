@@ -46,37 +46,22 @@ static inline float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo
 
 /* ------------------------------------------------------------------------------------ */
 /* deterministic sin (the float semantics of random(); see rt_oracle.h)                 */
+/* binary32 Cody-Waite reduction by pi/2 with a 3-part constant and explicit fmaf, then   */
+/* the Cephes sinf/cosf polynomials (public domain minimax coefficients).                */
 /* ------------------------------------------------------------------------------------ */
-/* pi/2 split for Cody-Waite: PIO2_1 = leading 33 bits, PIO2_2 next 33, PIO2_3 the tail
- * (fdlibm e_rem_pio2.c constants). */
-static const double RT_INV_PIO2 = 6.36619772367581382433e-01;
-static const double RT_PIO2_1 = 1.57079632673412561417e+00;
-static const double RT_PIO2_2 = 6.07710050630396597660e-11;
-static const double RT_PIO2_3 = 2.02226624879595063154e-21;
-/* fdlibm k_sin.c / k_cos.c minimax coefficients */
-static const double RT_S1 = -1.66666666666666324348e-01, RT_S2 = 8.33333333332248946124e-03,
-                    RT_S3 = -1.98412698298579493134e-04, RT_S4 = 2.75573137070700676789e-06,
-                    RT_S5 = -2.50507602534068634195e-08, RT_S6 = 1.58969099521155010221e-10;
-static const double RT_C1 = 4.16666666666666019037e-02, RT_C2 = -1.38888888888741095749e-03,
-                    RT_C3 = 2.48015872894767294178e-05, RT_C4 = -2.75573143513906633035e-07,
-                    RT_C5 = 2.08757232129817482790e-09, RT_C6 = -1.13596475577881948265e-11;
-
-float rto_sin(float xf) {
-  double x = (double)xf;
-  if (!(fabs(x) <= 3.4028234663852886e38)) return xf - xf; /* inf/nan -> nan */
-  double k = rint(x * RT_INV_PIO2);
-  double r = fma(-k, RT_PIO2_1, x);
-  r = fma(-k, RT_PIO2_2, r);
-  r = fma(-k, RT_PIO2_3, r);
-  double q4 = k - 4.0 * floor(k * 0.25); /* k mod 4, exact for |k| < 2^53 */
+float rto_sin(float x) {
+  if (!(fabsf(x) <= 3.40282347e38f)) return x - x; /* inf/nan -> nan */
+  float k = rintf(x * 0.636619772f);
+  float r = fmaf(-k, 1.57079637f, x);
+  r = fmaf(-k, -4.37113883e-08f, r);
+  r = fmaf(-k, -1.71512451e-15f, r);
+  float q4 = k - 4.0f * floorf(k * 0.25f); /* k mod 4, exact for |k| < 2^24 */
   int q = (int)q4;
-  double z = r * r;
-  double ps = fma(z, fma(z, fma(z, fma(z, fma(z, RT_S6, RT_S5), RT_S4), RT_S3), RT_S2), RT_S1);
-  double s = fma(r * z, ps, r);
-  double pc = fma(z, fma(z, fma(z, fma(z, fma(z, RT_C6, RT_C5), RT_C4), RT_C3), RT_C2), RT_C1);
-  double c = fma(z * z, pc, fma(-0.5, z, 1.0));
-  double v = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
-  return (float)v;
+  float z = r * r;
+  float s = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+  float c = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
+                 fmaf(-0.5f, z, 1.0f));
+  return (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
 }
 
 /* random(vec2) — p_compute.glsl:65-75: fract(sin(dot(st, vec2(12.9898,78.233))) * 43758.5453123) */

@@ -18,9 +18,10 @@
  *   - dot(a,b) = fmaf(a.z,b.z, fmaf(a.y,b.y, a.x*b.x)) (a fused chain, as GLSL compilers emit);
  *   - sphere discriminant = fmaf(r, r, fmaf(b, b, -dot(pmc,pmc)));
  *   - normalize(v) = v / sqrtf(dot(v,v)), length(v) = sqrtf(dot(v,v)), IEEE / and sqrtf;
- *   - sin() inside random() = rto_sin(): float -> double, Cody-Waite reduction by pi/2 and
- *     fdlibm kernel polynomials evaluated with explicit fma, rounded to float — a
- *     deterministic, correctly-rounded-in-practice sin both sides can reproduce bit for bit;
+ *   - sin() inside random() = rto_sin(): binary32 Cody-Waite reduction by pi/2 (3-part
+ *     constant, explicit fmaf) + Cephes sinf/cosf polynomials — a deterministic sin (abs
+ *     error ~1e-7 for |x| < 2^20) both sides reproduce bit for bit; random() only needs a
+ *     deterministic hash, and GLSL leaves sin's large-argument precision unspecified;
  *   - shadow_ray's `double t` and its dvec3 length run in binary64 (p_compute.glsl:147-163);
  *   - pow() = libm powf (outputs only; never feeds control flow), so pixels agree within
  *     the north-star tolerance |g-c| <= 1e-4*max(|g|,|c|) + 1e-6, not bit for bit.

@@ -33,34 +33,24 @@ __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; 
 __device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
 __device__ __forceinline__ float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
 
-// ---- deterministic sin: binary64 Cody-Waite reduction by pi/2 + fdlibm kernels ----------
-// (bit-identical to oracle/rt_oracle.c rto_sin; any finite float input)
-__device__ __forceinline__ float det_sin(float xf) {
-  constexpr double INV_PIO2 = 6.36619772367581382433e-01;
-  constexpr double PIO2_1 = 1.57079632673412561417e+00;
-  constexpr double PIO2_2 = 6.07710050630396597660e-11;
-  constexpr double PIO2_3 = 2.02226624879595063154e-21;
-  constexpr double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-                   S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-                   S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-  constexpr double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                   C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                   C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
-  double x = (double)xf;
-  if (!(fabs(x) <= 3.4028234663852886e38)) return xf - xf;
-  double k = rint(x * INV_PIO2);
-  double r = fma(-k, PIO2_1, x);
-  r = fma(-k, PIO2_2, r);
-  r = fma(-k, PIO2_3, r);
-  double q4 = k - 4.0 * floor(k * 0.25);
+// ---- deterministic sin: binary32 Cody-Waite reduction by pi/2 (3-part constant, explicit
+// fmaf) + Cephes sinf/cosf minimax polynomials.  Bit-identical to oracle/rt_oracle.c rto_sin
+// for every float input; |error| ~ 1e-7 absolute for |x| < 2^20 (random() arguments reach
+// ~5e5 at 8K).  GLSL leaves sin's precision for large arguments unspecified; what matters
+// for random() is that host and device compute the same value.
+__device__ __forceinline__ float det_sin(float x) {
+  if (!(fabsf(x) <= 3.40282347e38f)) return x - x;
+  float k = rintf(x * 0.636619772f);
+  float r = fmaf(-k, 1.57079637f, x);
+  r = fmaf(-k, -4.37113883e-08f, r);
+  r = fmaf(-k, -1.71512451e-15f, r);
+  float q4 = k - 4.0f * floorf(k * 0.25f);
   int q = (int)q4;
-  double z = r * r;
-  double ps = fma(z, fma(z, fma(z, fma(z, fma(z, S6, S5), S4), S3), S2), S1);
-  double s = fma(r * z, ps, r);
-  double pc = fma(z, fma(z, fma(z, fma(z, fma(z, C6, C5), C4), C3), C2), C1);
-  double c = fma(z * z, pc, fma(-0.5, z, 1.0));
-  double v = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
-  return (float)v;
+  float z = r * r;
+  float s = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+  float c = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
+                 fmaf(-0.5f, z, 1.0f));
+  return (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
 }
 
 // random(vec2), p_compute.glsl:65-75
@@ -145,6 +135,81 @@ __device__ __forceinline__ int closest_hit(const float4* __restrict__ geo, const
       }
     }
   }
+  t_out = t;
+  return ind;
+}
+
+// One ray-sphere candidate of the min-t scan: returns true (and updates t/ind) when sphere i
+// becomes the closest hit.  Equivalent to sphere_eval + the scan's acceptance test: a miss
+// (del < 0, or NaN) yields -1 / NaN in the reference, which the scan never accepts.
+__device__ __forceinline__ void sphere_candidate(f3 pos, f3 dir, float4 g, int i, float thr, float& t, int& ind) {
+  f3 pmc = pos - xyz(g);
+  float b = dot(dir, pmc);
+  float del = fmaf(g.w, g.w, fmaf(b, b, -dot(pmc, pmc)));
+  if (del >= 0.0f) {
+    float res;
+    if (del == 0.0f) {
+      res = -1.0f * b;
+    } else {
+      float s = sqrtf(del);
+      float t1 = -1.0f * b + s;
+      float t2 = -1.0f * b - s;
+      res = (t2 < 0.0f) ? ((t1 < 0.0f) ? -1.0f : t1) : t2;
+    }
+    if (res > thr && (res < t || t < 0.0f)) {
+      t = res;
+      ind = i;
+    }
+  }
+}
+
+// Variant of closest_hit for the A/B experiment: min-t update inside the hit branch and the
+// geometry of 4 spheres fetched before any of them is tested (V = 1: from LDS; V = 2: the
+// same table in global memory read with wave-uniform scalar loads).  Bit-identical results.
+template <bool ALLSPH, int V>
+__device__ __forceinline__ int closest_hit_v(const float4* __restrict__ geo, const float4* __restrict__ geo2,
+                                             int nobj, f3 pos, f3 dir, float thr, float& t_out) {
+  if (V == 0 || !ALLSPH) return closest_hit<ALLSPH>(geo, geo2, nobj, pos, dir, thr, t_out);
+  float t = -1.0f;
+  int ind = -1;
+  int i = 0;
+  for (; i + 4 <= nobj; i += 4) {
+    float4 g0 = geo[i], g1 = geo[i + 1], g2 = geo[i + 2], g3 = geo[i + 3];
+    sphere_candidate(pos, dir, g0, i, thr, t, ind);
+    sphere_candidate(pos, dir, g1, i + 1, thr, t, ind);
+    sphere_candidate(pos, dir, g2, i + 2, thr, t, ind);
+    sphere_candidate(pos, dir, g3, i + 3, thr, t, ind);
+  }
+  for (; i < nobj; ++i) sphere_candidate(pos, dir, geo[i], i, thr, t, ind);
+  t_out = t;
+  return ind;
+}
+
+// All-sphere closest hit with the scalar geometry loads software-pipelined: the next 4
+// spheres are requested before the current 4 are tested, so the scalar-cache latency overlaps
+// the tests.  Same visiting order and acceptance as closest_hit (bit-identical).
+__device__ __forceinline__ int closest_hit_pf(const float4* __restrict__ geo, int nobj, f3 pos, f3 dir, float thr,
+                                              float& t_out) {
+  float t = -1.0f;
+  int ind = -1;
+  int i = 0;
+  if (nobj >= 4) {
+    float4 g0 = geo[0], g1 = geo[1], g2 = geo[2], g3 = geo[3];
+    for (; i + 8 <= nobj; i += 4) {
+      float4 n0 = geo[i + 4], n1 = geo[i + 5], n2 = geo[i + 6], n3 = geo[i + 7];
+      sphere_candidate(pos, dir, g0, i, thr, t, ind);
+      sphere_candidate(pos, dir, g1, i + 1, thr, t, ind);
+      sphere_candidate(pos, dir, g2, i + 2, thr, t, ind);
+      sphere_candidate(pos, dir, g3, i + 3, thr, t, ind);
+      g0 = n0; g1 = n1; g2 = n2; g3 = n3;
+    }
+    sphere_candidate(pos, dir, g0, i, thr, t, ind);
+    sphere_candidate(pos, dir, g1, i + 1, thr, t, ind);
+    sphere_candidate(pos, dir, g2, i + 2, thr, t, ind);
+    sphere_candidate(pos, dir, g3, i + 3, thr, t, ind);
+    i += 4;
+  }
+  for (; i < nobj; ++i) sphere_candidate(pos, dir, geo[i], i, thr, t, ind);
   t_out = t;
   return ind;
 }

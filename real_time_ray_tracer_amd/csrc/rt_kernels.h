@@ -5,6 +5,8 @@
 namespace rt {
 
 constexpr int kMaxFrames = 16;
+constexpr int kCounters = 5;
+constexpr int kCounterSlots = 256;  // per counter, summed by the host
 
 // Everything one program launch needs.  Passed by value as the kernel argument (lives in the
 // kernarg segment -> SGPRs).  Row ranges are in frame coordinates (row 0 = bottom row).
@@ -33,7 +35,9 @@ struct FrameParams {
   const float4* hist_nrm[kMaxFrames];
   const float4* hist_dep[kMaxFrames];
   // optional work counters (nullptr in timed runs): [0] primary samples, [1] closest-hit
-  // segments, [2] shadow rays, [3] ray-shape tests = (segments + shadow rays) * nobj
+  // segments, [2] shadow rays, [3] ray-shape tests = (segments + shadow rays) * nobj,
+  // [4] executed lane-tests = sum over waves of 64 x (shapes tested by the wave's scene loops);
+  // each counter has kCounterSlots copies (index k * kCounterSlots + slot)
   unsigned long long* counters;
   // optional per-row closest-hit segment counts, indexed by (y - band_row0) (nullptr = off)
   unsigned long long* row_counters;

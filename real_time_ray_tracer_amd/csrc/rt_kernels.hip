@@ -13,6 +13,8 @@
 // sequential `result_color += ambient_occlusion(dir, aa)` (ao_compute.glsl:303-330).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "rt_device.h"
 #include "rt_kernels.h"
 
@@ -49,16 +51,34 @@ __device__ __forceinline__ void tile_xy(int& x, int& y, int row0) {
   y = row0 + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
 }
 
-// Work counters for the algorithmic-FLOP roofline (only when P.counters is set; the atomic
-// optimizer turns the uniform-address adds into one add per wave).
-__device__ __forceinline__ void count_work(const FrameParams& P, int y, unsigned samples, unsigned segs,
-                                           unsigned shadows) {
-  if (P.row_counters) atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)(segs + shadows));
+// Work counters for the algorithmic-FLOP roofline (only when P.counters is set).  Called by
+// every lane of a wave with the wave converged; one atomic per counter per wave.
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ unsigned wave_max(unsigned v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ void count_work(const FrameParams& P, bool active, int y, unsigned segs, unsigned shadows) {
+  if (P.row_counters && active) atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)(segs + shadows));
   if (!P.counters) return;
-  atomicAdd(&P.counters[0], (unsigned long long)samples);
-  atomicAdd(&P.counters[1], (unsigned long long)segs);
-  atomicAdd(&P.counters[2], (unsigned long long)shadows);
-  atomicAdd(&P.counters[3], (unsigned long long)(segs + shadows) * (unsigned long long)P.nobj);
+  if (!active) segs = shadows = 0;
+  unsigned n = wave_sum(active ? 1u : 0u), sg = wave_sum(segs), sh = wave_sum(shadows);
+  unsigned slots = wave_max(segs + shadows) * 64u;  // lane slots spent in scene loops (divergence)
+  if ((threadIdx.x & 63) == 0) {
+    // kCounterSlots copies per counter, spread by wave id, so waves do not serialise on one
+    // address; the host sums the slots
+    unsigned long long* c = P.counters + ((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kCounterSlots - 1));
+    atomicAdd(&c[0 * kCounterSlots], (unsigned long long)n);
+    atomicAdd(&c[1 * kCounterSlots], (unsigned long long)sg);
+    atomicAdd(&c[2 * kCounterSlots], (unsigned long long)sh);
+    atomicAdd(&c[3 * kCounterSlots], (unsigned long long)(sg + sh) * (unsigned long long)P.nobj);
+    atomicAdd(&c[4 * kCounterSlots], (unsigned long long)slots * (unsigned long long)P.nobj);
+  }
 }
 
 __device__ __forceinline__ void store_color(const FrameParams& P, int x, int y, float4 c) {
@@ -81,13 +101,22 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
   const float4 *geo = lds, *geo2 = lds + n, *col = lds + 2 * n;
   int x, y;
   tile_xy(x, y, P.trace_row0);
-  if (x >= P.W || y >= P.trace_row0 + P.trace_rows) return;
+  const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
+  if (P.counters || P.row_counters) {
+    unsigned hit = 0;
+    if (active) {
+      float t;
+      f3 d = primary_dir(P, (float)x / (float)P.W, (float)y / (float)P.H);
+      hit = closest_hit<ALLSPH>(geo, geo2, n, mk(P.cx, P.cy, P.cz), d, 0.0f, t) == -1 ? 0u : 1u;
+    }
+    count_work(P, active, y, 1u, hit);
+  }
+  if (!active) return;
 
   const f3 cam = mk(P.cx, P.cy, P.cz), light = mk(P.Lx, P.Ly, P.Lz);
   f3 dir = primary_dir(P, (float)x / (float)P.W, (float)y / (float)P.H);
   float t;
   int ind = closest_hit<ALLSPH>(geo, geo2, n, cam, dir, 0.0f, t);
-  count_work(P, y, 1u, 1u, ind == -1 ? 0u : 1u);
   float r, g, b;
   if (ind == -1) {
     r = P.bg.x; g = P.bg.y; b = P.bg.z;
@@ -122,8 +151,7 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
   const float4 *geo = lds, *geo2 = lds + n, *col = lds + 2 * n, *aux = lds + 3 * n;
   int x, y;
   tile_xy(x, y, P.trace_row0);
-  if (x >= P.W || y >= P.trace_row0 + P.trace_rows) return;
-
+  const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
   const f3 light = mk(P.Lx, P.Ly, P.Lz);
   f3 pos = mk(P.cx, P.cy, P.cz);
   f3 dir = primary_dir(P, (float)x / (float)P.W, (float)y / (float)P.H);
@@ -131,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
   float rr = 0, rg = 0, rb = 0;  // result_color.rgb
   float c = 0.0f;
   unsigned nseg = 0, nshadow = 0;
-  for (int seg = 0; seg < P.D; ++seg) {  // helper depth D, D-1, ..., 1
+  for (int seg = 0; active && seg < P.D; ++seg) {  // helper depth D, D-1, ..., 1
     // ---- hybrid_helper ----
     float t;
     int ind = closest_hit<ALLSPH>(geo, geo2, n, pos, dir, 0.001f, t);
@@ -181,8 +209,8 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
     }
     if (stop) break;
   }
-  count_work(P, y, 1u, nseg, nshadow);
-  store_color(P, x, y, gamma_out(0.0f + rr, 0.0f + rg, 0.0f + rb));
+  count_work(P, active, y, nseg, nshadow);
+  if (active) store_color(P, x, y, gamma_out(0.0f + rr, 0.0f + rg, 0.0f + rb));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -191,8 +219,8 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
 // ---------------------------------------------------------------------------------------
 enum { PRIM_HIT = 0, PRIM_MISS = 1, PRIM_EMISSIVE = 2 };
 
-template <bool ALLSPH>
-__global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P) {
+template <bool ALLSPH, int V>
+__global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4* __restrict__ gtab) {
   extern __shared__ float4 lds[];
   stage_shapes(P, lds);
   const int n = P.nobj;
@@ -213,6 +241,7 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P) {
   f3 n0 = mk(0.0f, 0.0f, 0.0f);
   float rr = 1.0f, rg = 1.0f, rb = 1.0f;
   float stopv = -1.0f;
+  unsigned nseg = 0;
   if (valid) {
     const float px = (float)x, py = (float)y;
     const float4* rbuf = P.rb;
@@ -242,10 +271,10 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P) {
     }
     const f3 cam = mk(P.cx, P.cy, P.cz);
     f3 pos = cam;
-    unsigned nseg = 0;
     for (int depth = P.D; depth > 0; --depth) {
       float t;
-      int ind = closest_hit<ALLSPH>(geo, geo2, n, pos, dir, 0.0001f, t);
+      int ind = V == 2 ? closest_hit_v<ALLSPH, 2>(gtab, gtab + P.S, n, pos, dir, 0.0001f, t)
+                       : closest_hit_v<ALLSPH, V>(geo, geo2, n, pos, dir, 0.0001f, t);
       ++nseg;
       if (ind != -1) {
         float4 att = col[ind];
@@ -282,8 +311,8 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P) {
         break;
       }
     }
-    count_work(P, y, 1u, nseg, 0u);
   }
+  count_work(P, valid, y, nseg, 0u);
   samp[threadIdx.x] = make_float4(rr, rg, rb, stopv);
   __syncthreads();
   if (!valid || aa != 0) return;
@@ -312,6 +341,566 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P) {
   d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
   P.dep[off] = d;
   store_color(P, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
+}
+
+// ---------------------------------------------------------------------------------------
+// modes 1/2 pass 1, pooled (all-sphere scenes).  One wave per workgroup owns a pool of
+// kPool pixel-samples: TP = kPool/spp consecutive pixels of the traced rows x spp samples.
+//  * path regeneration: a lane whose path ends takes the next sample of the pool, so the
+//    bounce rounds keep (nearly) every lane busy instead of waiting for the wave's longest
+//    path;
+//  * primary-ray culling: every primary ray starts at the camera and passes through the
+//    pool's pixel rectangle (jitter < 0.0834 px), so a sphere whose line distance from all
+//    rays of that frustum cone exceeds its radius by a float-error margin has a computed
+//    discriminant < 0 for every lane (-1 in the reference, never accepted) and is skipped.
+//    Survivors are tested in increasing index order, so ties resolve as in the reference.
+// Per-sample results go to LDS and are combined in sample order as in ao_kernel.
+// ---------------------------------------------------------------------------------------
+constexpr int kPool = 256;
+
+// Conservative cone around the primary rays of pixel rect [xmin,xmax] x [ymin,ymax].
+__device__ inline void pool_cone(const FrameParams& P, int xmin, int xmax, int ymin, int ymax, double a[3],
+                                 double& theta) {
+  const double hps[2] = {((double)xmin - 0.1) / P.W, ((double)xmax + 0.1) / P.W};
+  const double vps[2] = {((double)ymin - 0.1) / P.H, ((double)ymax + 0.1) / P.H};
+  double d[4][3], s[3] = {0.0, 0.0, 0.0};
+  for (int k = 0; k < 4; ++k) {
+    double hp = hps[k & 1], vp = vps[k >> 1];
+    double x = (double)P.lx + hp * P.hx + vp * P.vx;
+    double y = (double)P.ly + hp * P.hy + vp * P.vy;
+    double z = (double)P.lz + hp * P.hz + vp * P.vz;
+    double l = sqrt(x * x + y * y + z * z);
+    d[k][0] = x / l; d[k][1] = y / l; d[k][2] = z / l;
+    s[0] += d[k][0]; s[1] += d[k][1]; s[2] += d[k][2];
+  }
+  double l = sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
+  a[0] = s[0] / l; a[1] = s[1] / l; a[2] = s[2] / l;
+  double th = 0.0;
+  for (int k = 0; k < 4; ++k) {
+    double c = a[0] * d[k][0] + a[1] * d[k][1] + a[2] * d[k][2];
+    c = c > 1.0 ? 1.0 : (c < -1.0 ? -1.0 : c);
+    th = fmax(th, acos(c));
+  }
+  theta = th + 1e-5;  // + float error of the lanes' directions (~1e-6 rad)
+}
+
+// True when every ray from the camera inside the cone misses sphere g with a margin that
+// covers the float error of the discriminant: dist^2 sin^2(psi) > r^2 + 1e-5 (dist^2 + r^2)
+// for every angle psi between a ray and the centre direction (the computed del then stays
+// < 0; its error is below 2e-6 dist^2).
+__device__ inline bool cone_misses(const double a[3], double theta, float4 g, float cx, float cy, float cz) {
+  double Lx = (double)g.x - cx, Ly = (double)g.y - cy, Lz = (double)g.z - cz;
+  double d2 = Lx * Lx + Ly * Ly + Lz * Lz, r2 = (double)g.w * g.w;
+  if (!(d2 > r2 * 1.001 + 1e-6)) return false;  // camera inside / on the sphere: keep
+  double dist = sqrt(d2);
+  double c = (a[0] * Lx + a[1] * Ly + a[2] * Lz) / dist;
+  c = c > 1.0 ? 1.0 : (c < -1.0 ? -1.0 : c);
+  double phi = acos(c);
+  double lo = phi - theta;
+  if (!(lo > 1e-5)) return false;
+  double hi = fmin(3.141592653589793, phi + theta);
+  double sm = fmin(sin(lo), sin(hi));
+  return d2 * sm * sm > r2 + 1e-5 * (d2 + r2);
+}
+
+// Float form of the same cull (no trig): cone axis a, cos/sin of the half-angle; a sphere
+// with inflated radius r_eff (r_eff^2 = r^2 + 1e-5 (d^2 + r^2)) lies outside the forward and
+// the backward cone iff |cos phi| < cos(theta + alpha), sin alpha = r_eff / d.  Float error
+// (~1e-6) is covered by the 2e-5 slack on the cosine and the 1e-5 inflation.
+struct ConeF {
+  float ax, ay, az, ct, st;
+};
+
+__device__ inline ConeF pool_cone_f(const FrameParams& P, int xmin, int xmax, int ymin, int ymax) {
+  const float hps[2] = {((float)xmin - 0.1f) / P.W, ((float)xmax + 0.1f) / P.W};
+  const float vps[2] = {((float)ymin - 0.1f) / P.H, ((float)ymax + 0.1f) / P.H};
+  f3 d[4];
+  f3 sum = mk(0.0f, 0.0f, 0.0f);
+  for (int k = 0; k < 4; ++k) {
+    float hp = hps[k & 1], vp = vps[k >> 1];
+    f3 v = mk(P.lx + hp * P.hx + vp * P.vx, P.ly + hp * P.hy + vp * P.vy, P.lz + hp * P.hz + vp * P.vz);
+    float il = 1.0f / sqrtf(dot(v, v));
+    d[k] = il * v;
+    sum = sum + d[k];
+  }
+  float il = 1.0f / sqrtf(dot(sum, sum));
+  ConeF c;
+  c.ax = sum.x * il; c.ay = sum.y * il; c.az = sum.z * il;
+  float ct = 1.0f;
+  for (int k = 0; k < 4; ++k) ct = fminf(ct, c.ax * d[k].x + c.ay * d[k].y + c.az * d[k].z);
+  ct = fminf(fmaxf(ct - 2e-5f, -1.0f), 1.0f);  // widen the cone a little (direction rounding)
+  c.ct = ct;
+  c.st = sqrtf(fmaxf(0.0f, 1.0f - ct * ct));
+  return c;
+}
+
+__device__ inline bool cone_misses_f(const ConeF& c, float4 g, float cx, float cy, float cz) {
+  float Lx = g.x - cx, Ly = g.y - cy, Lz = g.z - cz;
+  float d2 = Lx * Lx + Ly * Ly + Lz * Lz, r2 = g.w * g.w;
+  float reff2 = r2 + 1e-5f * (d2 + r2);
+  if (!(d2 > reff2 * 1.01f + 1e-6f)) return false;  // camera inside / near the sphere: keep
+  float sa2 = reff2 / d2;
+  float sa = sqrtf(sa2), ca = sqrtf(1.0f - sa2);
+  float K = c.ct * ca - c.st * sa - 2e-5f;  // cos(theta + alpha), made smaller (conservative)
+  if (!(K > 0.0f)) return false;
+  float cphi = (c.ax * Lx + c.ay * Ly + c.az * Lz) / sqrtf(d2);
+  return fabsf(cphi) < K;
+}
+
+template <int MINW>
+__global__ __launch_bounds__(64, MINW) void ao_pool_kernel(FrameParams P, const float4* __restrict__ geo) {
+  extern __shared__ float4 lds[];
+  const int spp = P.spp, W = P.W, D = P.D, nobj = P.nobj;
+  const int TP = kPool / spp > 0 ? kPool / spp : 1;
+  const int lane = threadIdx.x;
+  float4* samp = lds;                      // [TP*spp] (r, g, b, stop value or -1)
+  float4* prec = lds + TP * spp;           // [TP] first-segment (normal, t) of sample 0
+  int* pkind = (int*)(prec + TP);          // [TP]
+  unsigned long long* cmask = (unsigned long long*)(pkind + ((TP + 1) & ~1));  // [ceil(nobj/64)]
+  const float4* col = P.shapes + 2 * P.S;
+  const float4* aux = P.shapes + 3 * P.S;
+
+  const long long npix = (long long)P.trace_rows * W;
+  const long long p0 = (long long)blockIdx.x * TP;
+  const int np = (int)(npix - p0 < TP ? npix - p0 : TP);
+  const int total = np * spp;
+
+  // ---- frustum cull of the primary rays -------------------------------------------------
+  const int yf = P.trace_row0 + (int)(p0 / W), xf = (int)(p0 % W);
+  const int yl = P.trace_row0 + (int)((p0 + np - 1) / W), xl = (int)((p0 + np - 1) % W);
+  double ca[3], th;
+  pool_cone(P, yf == yl ? xf : 0, yf == yl ? xl : W - 1, yf, yl, ca, th);
+  const int nwords = (nobj + 63) >> 6;
+  int ncull = 0;
+  for (int w = 0; w < nwords; ++w) {
+    int i = (w << 6) + lane;
+    bool keep = i < nobj && !cone_misses(ca, th, geo[i], P.cx, P.cy, P.cz);
+    unsigned long long m = __ballot(keep);
+    ncull += __popcll(m);
+    if (lane == 0) cmask[w] = m;
+  }
+  __syncthreads();
+
+  const f3 cam = mk(P.cx, P.cy, P.cz);
+  const float4* rbuf = P.rb;
+  int next = 0;            // wave-uniform: next pool sample
+  bool has = false;        // this lane holds a live path
+  int item = 0, depth = 0;
+  f3 pos = cam, dir = cam, hemi = cam;
+  float rr = 1.0f, rg = 1.0f, rb = 1.0f;
+  unsigned nseg = 0, sseg = 0;
+  unsigned long long exec_tests = 0;  // wave-uniform: shapes tested by the wave's loops
+
+  // One segment's bookkeeping (ao_compute.glsl:196-260 + ambient_occlusion 273-281).
+  auto segment = [&](int ind, float t) {
+    const int lp = item / spp, aa = item - lp * spp;
+    const bool first = depth == D;
+    ++nseg;
+    ++sseg;
+    float stopv = -2.0f;  // -2: path continues
+    if (ind != -1) {
+      float4 att = col[ind];
+      float4 ax = aux[ind];
+      if (ax.x > 0.9f) {
+        rr = rr * att.x; rg = rg * att.y; rb = rb * att.z;
+        stopv = (float)(D - depth);
+        if (aa == 0 && first) pkind[lp] = PRIM_EMISSIVE;
+      } else {
+        f3 curr = cam + t * dir;  // sic: camera origin (ao_compute.glsl:210)
+        f3 nn = normalize(curr - xyz(geo[ind]));
+        if (aa == 0 && first) {
+          pkind[lp] = PRIM_HIT;
+          prec[lp] = make_float4(nn.x, nn.y, nn.z, t);
+        }
+        rr = rr * att.x; rg = rg * att.y; rb = rb * att.z;
+        pos = curr;
+        float reflect = ax.y;
+        if (reflect > 0.999f) {
+          dir = normalize(hemi + nn);
+        } else {
+          float dn = dot(dir, nn);
+          f3 R = normalize(mk(dir.x - 2.0f * (dn * nn.x), dir.y - 2.0f * (dn * nn.y), dir.z - 2.0f * (dn * nn.z)));
+          dir = normalize(R + reflect * hemi);
+        }
+        depth -= 1;
+        if (depth == 0) stopv = -1.0f;  // RECURSION_DEPTH non-emissive hits: no stop write
+      }
+    } else {
+      if (aa == 0 && first) pkind[lp] = PRIM_MISS;
+      rr = rr * P.bg.x; rg = rg * P.bg.y; rb = rb * P.bg.z;
+      stopv = (float)(D - depth);
+    }
+    if (stopv != -2.0f) {
+      samp[item] = make_float4(rr, rg, rb, stopv);
+      if (P.row_counters) {
+        int y = P.trace_row0 + (int)((p0 + lp) / W);
+        atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)sseg);
+      }
+      has = false;
+    }
+  };
+
+  for (;;) {
+    // ---- refill idle lanes with new samples and trace their primary rays (culled set) ----
+    for (;;) {
+      unsigned long long need = __ballot(!has);
+      if (need == 0 || next >= total) break;
+      int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+      bool got = !has && next + rank < total;
+      int avail = total - next, want = __popcll(need);
+      if (got) item = next + rank;
+      next += want < avail ? want : avail;
+      exec_tests += (unsigned long long)ncull;
+      if (got) {
+        const int lp = item / spp, aa = item - lp * spp;
+        const long long pix = p0 + lp;
+        const int x = (int)(pix % W), y = P.trace_row0 + (int)(pix / W);
+        const float px = (float)x, py = (float)y;
+        float hp, vp;
+        if (aa == 0) {
+          hp = px / (float)W;
+          vp = py / (float)P.H;
+        } else {  // ao_compute.glsl:310-323
+          float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
+          float u = grandom(((s.x + px * f.z) - px) + f.x, ((f.y + py * s.w) - py) + s.y);
+          float w = grandom(s.z * px - (f.x * px) * f.z, f.w * py - (s.y * py) * s.w);
+          float l = sqrtf(fmaf(w, w, u * u));
+          hp = (px + ((u / l) / 6.0f - 0.08333f)) / (float)W;
+          vp = (py + ((w / l) / 6.0f - 0.08333f)) / (float)P.H;
+        }
+        dir = primary_dir(P, hp, vp);
+        {  // get_pt_within_unit_sphere(aa), hoisted (depends on aa and the pixel only)
+          float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
+          float a = grandom(f.x + px * s.z, f.y + py * s.w);
+          float b = grandom(f.z - px * s.z, f.w - py * s.w);
+          float e = grandom(s.x * px + s.z, s.y * py + s.w);
+          hemi = normalize(mk(a * 2.0f - 1.0f, b * 2.0f - 1.0f, e * 2.0f - 1.0f));
+        }
+        pos = cam;
+        rr = rg = rb = 1.0f;
+        depth = D;
+        sseg = 0;
+        has = true;
+        float t = -1.0f;
+        int ind = -1;
+        for (int w = 0; w < nwords; ++w) {
+          unsigned long long m = cmask[w];
+          m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
+              (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
+          while (m) {
+            int i = (w << 6) + __builtin_ctzll(m);
+            m &= m - 1;
+            sphere_candidate(pos, dir, geo[i], i, 0.0001f, t, ind);
+          }
+        }
+        segment(ind, t);
+      }
+    }
+    if (__ballot(has) == 0) break;
+    // ---- one bounce segment for every live path, against every sphere ------------------
+    exec_tests += (unsigned long long)nobj;
+    if (has) {
+      float t;
+      int ind = closest_hit_v<true, 2>(geo, geo, nobj, pos, dir, 0.0001f, t);
+      segment(ind, t);
+    }
+  }
+
+  if (P.counters) {
+    unsigned sg = wave_sum(nseg);
+    if (lane == 0) {
+      unsigned long long* c = P.counters + (blockIdx.x & (kCounterSlots - 1));
+      atomicAdd(&c[0 * kCounterSlots], (unsigned long long)total);
+      atomicAdd(&c[1 * kCounterSlots], (unsigned long long)sg);
+      atomicAdd(&c[3 * kCounterSlots], (unsigned long long)sg * (unsigned long long)nobj);
+      atomicAdd(&c[4 * kCounterSlots], 64ull * exec_tests);
+    }
+  }
+  __syncthreads();
+
+  // ---- sample combine in aa order (ao_compute.glsl:303-339) ----------------------------
+  for (int lp = lane; lp < np; lp += 64) {
+    const long long pix = p0 + lp;
+    const int x = (int)(pix % W), y = P.trace_row0 + (int)(pix / W);
+    float sr = 0.0f, sg = 0.0f, sb = 0.0f, ystop = -1.0f;
+    const float4* ps = samp + lp * spp;
+    for (int k = 0; k < spp; ++k) {
+      float4 q = ps[k];
+      sr = sr + q.x; sg = sg + q.y; sb = sb + q.z;
+      if (q.w >= 0.0f) ystop = q.w;
+    }
+    const float fa = (float)spp;
+    const size_t off = (size_t)(y - P.band_row0) * W + x;
+    const int kind = pkind[lp];
+    float4 d;
+    if (kind == PRIM_HIT) {
+      float4 r0 = prec[lp];
+      d = make_float4(r0.w, 0.0f, 0.0f, 1.0f);
+      P.nrm[off] = make_float4(r0.x, r0.y, r0.z, 1.0f);
+    } else if (kind == PRIM_MISS) {
+      d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      P.nrm[off] = d;
+    } else {
+      d = P.dep[off];
+    }
+    if (ystop >= 0.0f) d.y = ystop;
+    d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
+    P.dep[off] = d;
+    store_color(P, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Pooled AO, batch-prepared (variant 6).  As ao_pool_kernel, but new samples are prepared 64
+// at a time with the whole wave active: primary direction + hemisphere vector + primary hit
+// over the culled set + first-hit shading.  Samples whose path ended at the primary hit are
+// final at once; the live post-primary states are kept in the lanes that prepared them and
+// handed to idle lanes by ds_bpermute whenever lanes run out of work.  Bounce rounds then
+// run with (nearly) all lanes live, and no per-sample setup runs at partial utilisation.
+// ---------------------------------------------------------------------------------------
+template <int MINW>
+__global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
+  extern __shared__ float4 lds[];
+  const int spp = P.spp, W = P.W, D = P.D, nobj = P.nobj;
+  const int TP = kPool / spp > 0 ? kPool / spp : 1;
+  const int lane = threadIdx.x;
+  float4* samp = lds;                      // [TP*spp] (r, g, b, stop value or -1)
+  float4* prec = lds + TP * spp;           // [TP] first-segment (normal, t) of sample 0
+  int* pkind = (int*)(prec + TP);          // [TP]
+  int* perm = pkind + ((TP + 1) & ~1);     // [64] live-rank -> lane of the prepared batch
+  unsigned long long* cmask = (unsigned long long*)(perm + 64);  // [ceil(nobj/64)]
+  const float4* col = P.shapes + 2 * P.S;
+  const float4* aux = P.shapes + 3 * P.S;
+
+  const long long npix = (long long)P.trace_rows * W;
+  const long long p0 = (long long)blockIdx.x * TP;
+  const int np = (int)(npix - p0 < TP ? npix - p0 : TP);
+  const int total = np * spp;
+
+  // ---- frustum cull of the primary rays -------------------------------------------------
+  const int yf = P.trace_row0 + (int)(p0 / W), xf = (int)(p0 % W);
+  const int yl = P.trace_row0 + (int)((p0 + np - 1) / W), xl = (int)((p0 + np - 1) % W);
+  int ncull = 0;
+  const int nwords = (nobj + 63) >> 6;
+  {
+    const ConeF cone = pool_cone_f(P, yf == yl ? xf : 0, yf == yl ? xl : W - 1, yf, yl);
+    for (int w = 0; w < nwords; ++w) {
+      int i = (w << 6) + lane;
+      bool keep = i < nobj && !cone_misses_f(cone, geo[i], P.cx, P.cy, P.cz);
+      unsigned long long m = __ballot(keep);
+      ncull += __popcll(m);
+      if (lane == 0) cmask[w] = m;
+    }
+  }
+  __syncthreads();
+
+  const f3 cam = mk(P.cx, P.cy, P.cz);
+  const float4* rbuf = P.rb;
+  // live path of this lane
+  bool has = false;
+  int item = 0, depth = 0;
+  f3 pos = cam, dir = cam, hemi = cam;
+  float rr = 1.0f, rg = 1.0f, rb = 1.0f;
+  // prepared batch slot of this lane
+  int bitem = 0;
+  f3 bpos = cam, bdir = cam, bhemi = cam;
+  float br = 1.0f, bg = 1.0f, bb = 1.0f;
+  int next = 0, cursor = 0, nlive = 0;  // wave-uniform
+  unsigned nseg = 0;
+  unsigned long long exec_tests = 0;
+
+  const float inv_spp = 1.0f / (float)spp;
+  // it / spp for pool items (< 2^16): exact via the float reciprocal (error << 0.5/spp)
+  auto div_spp = [&](int it) { return (int)(((float)it + 0.5f) * inv_spp); };
+  auto finish = [&](int it, float r, float g, float b, float stopv, int segs) {
+    samp[it] = make_float4(r, g, b, stopv);
+    if (P.row_counters) {
+      int y = P.trace_row0 + (int)((p0 + div_spp(it)) / W);
+      atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)segs);
+    }
+  };
+
+  // hit shading shared by primary and bounce segments; returns true when the path goes on
+  auto shade = [&](int ind, float t, f3& ps, f3& dr, f3 hm, float& r, float& g, float& b, int dpt, int it,
+                   bool first) -> bool {
+    const int lp = div_spp(it), aa = it - lp * spp;
+    if (ind != -1) {
+      float4 att = col[ind];
+      float4 ax = aux[ind];
+      if (ax.x > 0.9f) {
+        r = r * att.x; g = g * att.y; b = b * att.z;
+        if (aa == 0 && first) pkind[lp] = PRIM_EMISSIVE;
+        finish(it, r, g, b, (float)(D - dpt), D - dpt + 1);
+        return false;
+      }
+      f3 curr = cam + t * dr;  // sic: camera origin (ao_compute.glsl:210)
+      f3 nn = normalize(curr - xyz(geo[ind]));
+      if (aa == 0 && first) {
+        pkind[lp] = PRIM_HIT;
+        prec[lp] = make_float4(nn.x, nn.y, nn.z, t);
+      }
+      r = r * att.x; g = g * att.y; b = b * att.z;
+      ps = curr;
+      float reflect = ax.y;
+      if (reflect > 0.999f) {
+        dr = normalize(hm + nn);
+      } else {
+        float dn = dot(dr, nn);
+        f3 R = normalize(mk(dr.x - 2.0f * (dn * nn.x), dr.y - 2.0f * (dn * nn.y), dr.z - 2.0f * (dn * nn.z)));
+        dr = normalize(R + reflect * hm);
+      }
+      if (dpt - 1 == 0) {  // RECURSION_DEPTH non-emissive hits: no stop write
+        finish(it, r, g, b, -1.0f, D);
+        return false;
+      }
+      return true;
+    }
+    if (aa == 0 && first) pkind[lp] = PRIM_MISS;
+    r = r * P.bg.x; g = g * P.bg.y; b = b * P.bg.z;
+    finish(it, r, g, b, (float)(D - dpt), D - dpt + 1);
+    return false;
+  };
+
+  // Prepare the next 64 samples with the whole wave.
+  auto prepare = [&]() {
+    bitem = next + lane;
+    bool live = false;
+    exec_tests += (unsigned long long)ncull;
+    if (bitem < total) {
+      const int lp = div_spp(bitem), aa = bitem - lp * spp;
+      const long long pix = p0 + lp;
+      const int x = (int)(pix % W), y = P.trace_row0 + (int)(pix / W);
+      const float px = (float)x, py = (float)y;
+      float hp, vp;
+      if (aa == 0) {
+        hp = px / (float)W;
+        vp = py / (float)P.H;
+      } else {  // ao_compute.glsl:310-323
+        float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
+        float u = grandom(((s.x + px * f.z) - px) + f.x, ((f.y + py * s.w) - py) + s.y);
+        float w = grandom(s.z * px - (f.x * px) * f.z, f.w * py - (s.y * py) * s.w);
+        float l = sqrtf(fmaf(w, w, u * u));
+        hp = (px + ((u / l) / 6.0f - 0.08333f)) / (float)W;
+        vp = (py + ((w / l) / 6.0f - 0.08333f)) / (float)P.H;
+      }
+      bdir = primary_dir(P, hp, vp);
+      {  // get_pt_within_unit_sphere(aa), hoisted (depends on aa and the pixel only)
+        float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
+        float a = grandom(f.x + px * s.z, f.y + py * s.w);
+        float b = grandom(f.z - px * s.z, f.w - py * s.w);
+        float e = grandom(s.x * px + s.z, s.y * py + s.w);
+        bhemi = normalize(mk(a * 2.0f - 1.0f, b * 2.0f - 1.0f, e * 2.0f - 1.0f));
+      }
+      bpos = cam;
+      br = bg = bb = 1.0f;
+      float t = -1.0f;
+      int ind = -1;
+      for (int w = 0; w < nwords; ++w) {
+        unsigned long long m = cmask[w];
+        m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
+            (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
+        while (m) {
+          int i = (w << 6) + __builtin_ctzll(m);
+          m &= m - 1;
+          sphere_candidate(bpos, bdir, geo[i], i, 0.0001f, t, ind);
+        }
+      }
+      ++nseg;
+      live = shade(ind, t, bpos, bdir, bhemi, br, bg, bb, D, bitem, true);
+    }
+    unsigned long long lm = __ballot(live);
+    if (live) perm[__builtin_amdgcn_mbcnt_hi((unsigned)(lm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)lm, 0u))] = lane;
+    nlive = __popcll(lm);
+    cursor = 0;
+    next = next + 64 < total ? next + 64 : total;
+    __syncthreads();  // perm[] visible to the whole wave
+  };
+
+  for (;;) {
+    // ---- hand prepared live states to idle lanes; prepare more when the batch is used up --
+    for (;;) {
+      unsigned long long need = __ballot(!has);
+      if (need == 0) break;
+      if (cursor >= nlive) {
+        if (next >= total) break;
+        prepare();
+        continue;
+      }
+      int r = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+      int take = __popcll(need) < nlive - cursor ? __popcll(need) : nlive - cursor;
+      bool get = !has && r < take;
+      int src = get ? perm[cursor + r] : lane;
+      // every lane executes the shuffles (ds_bpermute reads the source lane's register)
+      float sx = __shfl(bpos.x, src), sy = __shfl(bpos.y, src), sz = __shfl(bpos.z, src);
+      float dx = __shfl(bdir.x, src), dy = __shfl(bdir.y, src), dz = __shfl(bdir.z, src);
+      float hx = __shfl(bhemi.x, src), hy = __shfl(bhemi.y, src), hz = __shfl(bhemi.z, src);
+      float cr = __shfl(br, src), cg = __shfl(bg, src), cb = __shfl(bb, src);
+      int ci = __shfl(bitem, src);
+      if (get) {
+        pos = mk(sx, sy, sz);
+        dir = mk(dx, dy, dz);
+        hemi = mk(hx, hy, hz);
+        rr = cr; rg = cg; rb = cb;
+        item = ci;
+        depth = D - 1;
+        has = true;
+      }
+      cursor += take;
+    }
+    if (__ballot(has) == 0) break;
+    // ---- one bounce segment for every live path, against every sphere ------------------
+    exec_tests += (unsigned long long)nobj;
+    if (has) {
+      float t;
+      int ind = closest_hit_pf(geo, nobj, pos, dir, 0.0001f, t);
+      ++nseg;
+      has = shade(ind, t, pos, dir, hemi, rr, rg, rb, depth, item, false);
+      depth -= 1;
+    }
+  }
+
+  if (P.counters) {
+    unsigned sg = wave_sum(nseg);
+    if (lane == 0) {
+      unsigned long long* c = P.counters + (blockIdx.x & (kCounterSlots - 1));
+      atomicAdd(&c[0 * kCounterSlots], (unsigned long long)total);
+      atomicAdd(&c[1 * kCounterSlots], (unsigned long long)sg);
+      atomicAdd(&c[3 * kCounterSlots], (unsigned long long)sg * (unsigned long long)nobj);
+      atomicAdd(&c[4 * kCounterSlots], 64ull * exec_tests);
+    }
+  }
+  __syncthreads();
+
+  // ---- sample combine in aa order (ao_compute.glsl:303-339) ----------------------------
+  for (int lp = lane; lp < np; lp += 64) {
+    const long long pix = p0 + lp;
+    const int x = (int)(pix % W), y = P.trace_row0 + (int)(pix / W);
+    float sr = 0.0f, sg = 0.0f, sb = 0.0f, ystop = -1.0f;
+    const float4* ps = samp + lp * spp;
+    for (int k = 0; k < spp; ++k) {
+      float4 q = ps[k];
+      sr = sr + q.x; sg = sg + q.y; sb = sb + q.z;
+      if (q.w >= 0.0f) ystop = q.w;
+    }
+    const float fa = (float)spp;
+    const size_t off = (size_t)(y - P.band_row0) * W + x;
+    const int kind = pkind[lp];
+    float4 d;
+    if (kind == PRIM_HIT) {
+      float4 r0 = prec[lp];
+      d = make_float4(r0.w, 0.0f, 0.0f, 1.0f);
+      P.nrm[off] = make_float4(r0.x, r0.y, r0.z, 1.0f);
+    } else if (kind == PRIM_MISS) {
+      d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      P.nrm[off] = d;
+    } else {
+      d = P.dep[off];
+    }
+    if (ystop >= 0.0f) d.y = ystop;
+    d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
+    P.dep[off] = d;
+    store_color(P, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -422,10 +1011,33 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
     const long long npix = (long long)p.trace_rows * p.W;
     const long long grid = (npix + ppb - 1) / ppb;
     const size_t sh = lds + (size_t)block * sizeof(float4);
-    if (all_spheres)
-      hipLaunchKernelGGL(ao_kernel<true>, dim3((unsigned)grid), dim3(block), sh, stream, p);
+    // RTRT_AO_VARIANT: internal A/B switch for kernel experiments (tools/ab.py); the default
+    // is the pooled, batch-prepared kernel (7) for all-sphere scenes.
+    const char* ev = getenv("RTRT_AO_VARIANT");
+    const int variant = ev ? atoi(ev) : 7;
+    if (all_spheres && variant >= 3) {
+      const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
+      const long long pools = (npix + TP - 1) / TP;
+      const size_t psh = (size_t)TP * p.spp * sizeof(float4) + (size_t)TP * sizeof(float4) +
+                         (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 1) * 8;
+      if (variant == 6)
+        hipLaunchKernelGGL(ao_batch_kernel<1>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+      else if (variant == 7)
+        hipLaunchKernelGGL(ao_batch_kernel<6>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+      else if (variant == 4)
+        hipLaunchKernelGGL(ao_pool_kernel<8>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+      else if (variant == 5)
+        hipLaunchKernelGGL(ao_pool_kernel<6>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+      else
+        hipLaunchKernelGGL(ao_pool_kernel<1>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+    } else if (!all_spheres)
+      hipLaunchKernelGGL((ao_kernel<false, 0>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
+    else if (variant == 1)
+      hipLaunchKernelGGL((ao_kernel<true, 1>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
+    else if (variant == 2)
+      hipLaunchKernelGGL((ao_kernel<true, 2>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
     else
-      hipLaunchKernelGGL(ao_kernel<false>, dim3((unsigned)grid), dim3(block), sh, stream, p);
+      hipLaunchKernelGGL((ao_kernel<true, 0>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
     return hipGetLastError();
   }
   dim3 grid((p.W + 15) / 16, (p.trace_rows + 15) / 16);

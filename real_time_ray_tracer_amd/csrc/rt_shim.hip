@@ -68,6 +68,7 @@ struct rt_ctx {
   unsigned long long* d_counters = nullptr;
   unsigned long long* d_row_counters = nullptr;  // [band_rows]
   bool counting = false;
+  bool row_counting = false;
   int last_hip = 0;
 };
 
@@ -176,7 +177,7 @@ void fill_params(const rt_ctx* c, int frame, rt::FrameParams& p) {
   p.nrm = c->nrm[frame];
   p.dep = c->dep[frame];
   p.counters = c->counting ? c->d_counters : nullptr;
-  p.row_counters = c->counting ? c->d_row_counters : nullptr;
+  p.row_counters = c->row_counting ? c->d_row_counters : nullptr;
 }
 
 int launch(rt_ctx* c, int program, const rt::FrameParams& p) {
@@ -568,27 +569,33 @@ int rt_enable_counters(rt_ctx* c, int on) {
   if (!c) return RT_E_INVAL;
   RT_HIP(c, hipSetDevice(c->device));
   if (on && !c->d_counters) {
-    RT_HIP(c, hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long)));
-    RT_HIP(c, hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
+    RT_HIP(c, hipMalloc(&c->d_counters, rt::kCounters * rt::kCounterSlots * sizeof(unsigned long long)));
+    RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kCounters * rt::kCounterSlots * sizeof(unsigned long long),
+                             c->stream));
     RT_HIP(c, hipMalloc(&c->d_row_counters, (size_t)c->band_rows * sizeof(unsigned long long)));
     RT_HIP(c, hipMemsetAsync(c->d_row_counters, 0, (size_t)c->band_rows * sizeof(unsigned long long), c->stream));
   }
-  c->counting = on != 0;
+  c->counting = (on & 1) != 0;
+  c->row_counting = (on & 2) != 0;
   return RT_OK;
 }
 
-int rt_read_counters(rt_ctx* c, uint64_t out[4], int reset) {
+int rt_read_counters(rt_ctx* c, uint64_t out[5], int reset) {
   if (!c || !out) return RT_E_INVAL;
   if (!c->d_counters) {
-    for (int k = 0; k < 4; ++k) out[k] = 0;
+    for (int k = 0; k < rt::kCounters; ++k) out[k] = 0;
     return RT_OK;
   }
   RT_HIP(c, hipSetDevice(c->device));
-  unsigned long long h[4];
+  std::vector<unsigned long long> h((size_t)rt::kCounters * rt::kCounterSlots);
   RT_HIP(c, hipStreamSynchronize(c->stream));
-  RT_HIP(c, hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
-  for (int k = 0; k < 4; ++k) out[k] = (uint64_t)h[k];
-  if (reset) RT_HIP(c, hipMemset(c->d_counters, 0, sizeof(h)));
+  RT_HIP(c, hipMemcpy(h.data(), c->d_counters, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  for (int k = 0; k < rt::kCounters; ++k) {
+    unsigned long long sum = 0;
+    for (int j = 0; j < rt::kCounterSlots; ++j) sum += h[(size_t)k * rt::kCounterSlots + j];
+    out[k] = (uint64_t)sum;
+  }
+  if (reset) RT_HIP(c, hipMemset(c->d_counters, 0, h.size() * sizeof(unsigned long long)));
   return RT_OK;
 }
 

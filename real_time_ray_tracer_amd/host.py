@@ -272,13 +272,14 @@ class Renderer:
     def reset_stats(self):
         self._c(self._lib.rt_reset_stats(self.ctx), "rt_reset_stats")
 
-    def enable_counters(self, on: bool = True):
-        self._c(self._lib.rt_enable_counters(self.ctx, int(on)), "rt_enable_counters")
+    def enable_counters(self, totals: bool = True, rows: bool = False):
+        self._c(self._lib.rt_enable_counters(self.ctx, int(totals) | (2 if rows else 0)), "rt_enable_counters")
 
     def read_counters(self, reset: bool = True) -> dict:
-        out = (C.c_uint64 * 4)()
+        out = (C.c_uint64 * 5)()
         self._c(self._lib.rt_read_counters(self.ctx, out, int(reset)), "rt_read_counters")
-        return {"samples": out[0], "segments": out[1], "shadow_rays": out[2], "tests": out[3]}
+        return {"samples": out[0], "segments": out[1], "shadow_rays": out[2], "tests": out[3],
+                "executed_lane_tests": out[4]}
 
     def read_row_counters(self, reset: bool = True) -> np.ndarray:
         out = np.zeros(self.R, np.uint64)

@@ -1,0 +1,74 @@
+#!/usr/bin/env python
+"""Interleaved A/B timing of kernel variants in one process (cdna_hip_programming.md §5.4
+rule 24).  Each round renders the same frames once per variant (env RTRT_AO_VARIANT, read by
+the shim at launch) and records the per-launch HIP-event time of the trace kernel; images
+must be bit-identical across variants.
+
+    python tools/ab.py --config d --variants 0,1,2 --rounds 3 --frames 4
+"""
+import argparse
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+from bench import CONFIG_INDEX, CONFIGS  # noqa: E402
+from real_time_ray_tracer_amd import Header, Renderer, aspect_for  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="d")
+    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=4)
+    ap.add_argument("--env", default="RTRT_AO_VARIANT")
+    args = ap.parse_args()
+    W, H, S, spp, mode, desc = CONFIGS[args.config]
+    variants = [v for v in args.variants.split(",")]
+    h = Header.synthetic(S, spp, 1234 + CONFIG_INDEX[args.config], aspect_for(W, H))
+    prog = {1: 1, 2: 3, 3: 4, 4: 5}[mode]
+    times = {v: [] for v in variants}
+    ref_img = None
+    counts = None
+    for rnd in range(args.rounds):
+        for v in variants:
+            os.environ[args.env] = v
+            r = Renderer(W, H, S, spp)
+            if rnd == 0 and v == variants[0]:
+                r.enable_counters(True)
+            f = 0
+            for k in range(args.frames):
+                h.fill_rand_buffer(7000 + k)
+                h.set_mode(f, S)
+                r.upload_header(h)
+                if k == 1:
+                    r.enable_timing(True)
+                f = r.dispatch(mode, f)
+            n, ms = r.kernel_stats(prog)
+            times[v].append(ms / n)
+            if rnd == 0 and v == variants[0]:
+                counts = r.read_counters()
+            img = r.image()
+            if ref_img is None:
+                ref_img = img
+            same = np.array_equal(img.view(np.uint32), ref_img.view(np.uint32))
+            print(f"round {rnd} variant {v}: {ms / n:.3f} ms/launch identical={same}", flush=True)
+            if not same:
+                raise SystemExit(f"variant {v} changed the image")
+            r.close()
+    out = {"config": desc, "counters": counts,
+           "ms": {v: {"median": float(np.median(t)), "min": float(np.min(t))} for v, t in times.items()}}
+    if counts:
+        out["lane_utilisation"] = counts["tests"] / max(counts["executed_lane_tests"], 1)
+        out["segments_per_sample"] = counts["segments"] / max(counts["samples"], 1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
