@@ -34,10 +34,11 @@ static inline v3 add3(v3 a, v3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z);
 static inline v3 scl3(float s, v3 v) { return mk3(s * v.x, s * v.y, s * v.z); }
 /* GLSL dot(): fused chain */
 static inline float dot3(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
-/* GLSL normalize(): v / length(v) */
+/* GLSL normalize(): v * (1 / length(v)) — the correctly rounded form of the reciprocal-
+ * square-root multiply GPU GLSL compilers emit */
 static inline v3 nrm3(v3 v) {
-  float l = sqrtf(dot3(v, v));
-  return mk3(v.x / l, v.y / l, v.z / l);
+  float il = 1.0f / sqrtf(dot3(v, v));
+  return mk3(v.x * il, v.y * il, v.z * il);
 }
 /* GLSL min/max/clamp definitions (GLSL 4.60 §8.3): max(x,y) = x < y ? y : x, etc. */
 static inline float gmax(float x, float y) { return x < y ? y : x; }
@@ -468,9 +469,9 @@ static void ao_main(octx* c, int x, int y, float* image, int write_image) {
     float s4x = s[2], s4y = f[3]; /* seed4 = (rb[second].z, rb[first].w) */
     float u = rto_random(((s1x + px * s2x) - px) + s3x, ((s1y + py * s2y) - py) + s3y);
     float w = rto_random(s4x * px - (s3x * px) * s2x, s4y * py - (s3y * py) * s2y);
-    float l = sqrtf(fmaf(w, w, u * u));
-    float jx = (u / l) / 6.0f - 0.08333f;
-    float jy = (w / l) / 6.0f - 0.08333f;
+    float il = 1.0f / sqrtf(fmaf(w, w, u * u)); /* normalize(vec2) */
+    float jx = (u * il) / 6.0f - 0.08333f;
+    float jy = (w * il) / 6.0f - 0.08333f;
     float hp = (px + jx) / (float)c->d->W;
     float vp = (py + jy) / (float)c->d->H;
     v4 r = ambient_occlusion(c, primary_dir(c, hp, vp), aa, x, y);

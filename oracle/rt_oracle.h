@@ -17,7 +17,8 @@
  *     (built with -ffp-contract=off); operations in the written GLSL order;
  *   - dot(a,b) = fmaf(a.z,b.z, fmaf(a.y,b.y, a.x*b.x)) (a fused chain, as GLSL compilers emit);
  *   - sphere discriminant = fmaf(r, r, fmaf(b, b, -dot(pmc,pmc)));
- *   - normalize(v) = v / sqrtf(dot(v,v)), length(v) = sqrtf(dot(v,v)), IEEE / and sqrtf;
+ *   - normalize(v) = v * (1.0f / sqrtf(dot(v,v))), length(v) = sqrtf(dot(v,v)), IEEE / and
+ *     sqrtf (the correctly rounded form of the rsqrt-multiply GLSL compilers emit);
  *   - sin() inside random() = rto_sin(): binary32 Cody-Waite reduction by pi/2 (3-part
  *     constant, explicit fmaf) + Cephes sinf/cosf polynomials — a deterministic sin (abs
  *     error ~1e-7 for |x| < 2^20) both sides reproduce bit for bit; random() only needs a

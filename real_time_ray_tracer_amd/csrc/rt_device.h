@@ -2,7 +2,7 @@
 //
 // Implements the float semantics documented in oracle/rt_oracle.h (the contract the CPU
 // oracle and these kernels share): IEEE binary32, no implicit contraction (the library is
-// built with -ffp-contract=off), dot() as a fused chain, IEEE sqrtf and '/', the
+// built with -ffp-contract=off), dot() as a fused chain, normalize = v * (1/sqrtf(dot)), the
 // deterministic binary64 sin inside random(), binary64 shadow-ray distance test.
 // Reference: resources/p_compute.glsl:65-166, ao_compute.glsl:143-158.
 #pragma once
@@ -23,10 +23,17 @@ __device__ __forceinline__ f3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
 
 // GLSL dot(): fmaf(a.z,b.z, fmaf(a.y,b.y, a.x*b.x))
 __device__ __forceinline__ float dot(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
-// GLSL normalize(): v / length(v) with IEEE sqrt and division
+// GLSL normalize(): v * (1 / length(v)) with IEEE sqrt and division (GPU GLSL compilers
+// lower normalize to a reciprocal-square-root multiply; this is its correctly rounded form)
 __device__ __forceinline__ f3 normalize(f3 v) {
-  float l = sqrtf(dot(v, v));
-  return mk(v.x / l, v.y / l, v.z / l);
+  float il = 1.0f / sqrtf(dot(v, v));
+  return mk(v.x * il, v.y * il, v.z * il);
+}
+// GLSL normalize(vec2)
+__device__ __forceinline__ void normalize2(float& x, float& y) {
+  float il = 1.0f / sqrtf(fmaf(y, y, x * x));
+  x = x * il;
+  y = y * il;
 }
 // GLSL 4.60 §8.3 definitions: max(x,y) = x < y ? y : x; min(x,y) = y < x ? y : x
 __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; }

@@ -253,9 +253,9 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4*
       float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
       float u = grandom(((s.x + px * f.z) - px) + f.x, ((f.y + py * s.w) - py) + s.y);
       float w = grandom(s.z * px - (f.x * px) * f.z, f.w * py - (s.y * py) * s.w);
-      float l = sqrtf(fmaf(w, w, u * u));
-      float jx = (u / l) / 6.0f - 0.08333f;
-      float jy = (w / l) / 6.0f - 0.08333f;
+      normalize2(u, w);
+      float jx = u / 6.0f - 0.08333f;
+      float jy = w / 6.0f - 0.08333f;
       hp = (px + jx) / (float)P.W;
       vp = (py + jy) / (float)P.H;
     }
@@ -564,9 +564,9 @@ __global__ __launch_bounds__(64, MINW) void ao_pool_kernel(FrameParams P, const 
           float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
           float u = grandom(((s.x + px * f.z) - px) + f.x, ((f.y + py * s.w) - py) + s.y);
           float w = grandom(s.z * px - (f.x * px) * f.z, f.w * py - (s.y * py) * s.w);
-          float l = sqrtf(fmaf(w, w, u * u));
-          hp = (px + ((u / l) / 6.0f - 0.08333f)) / (float)W;
-          vp = (py + ((w / l) / 6.0f - 0.08333f)) / (float)P.H;
+          normalize2(u, w);
+          hp = (px + (u / 6.0f - 0.08333f)) / (float)W;
+          vp = (py + (w / 6.0f - 0.08333f)) / (float)P.H;
         }
         dir = primary_dir(P, hp, vp);
         {  // get_pt_within_unit_sphere(aa), hoisted (depends on aa and the pixel only)
@@ -779,9 +779,9 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
         float u = grandom(((s.x + px * f.z) - px) + f.x, ((f.y + py * s.w) - py) + s.y);
         float w = grandom(s.z * px - (f.x * px) * f.z, f.w * py - (s.y * py) * s.w);
-        float l = sqrtf(fmaf(w, w, u * u));
-        hp = (px + ((u / l) / 6.0f - 0.08333f)) / (float)W;
-        vp = (py + ((w / l) / 6.0f - 0.08333f)) / (float)P.H;
+        normalize2(u, w);
+        hp = (px + (u / 6.0f - 0.08333f)) / (float)W;
+        vp = (py + (w / 6.0f - 0.08333f)) / (float)P.H;
       }
       bdir = primary_dir(P, hp, vp);
       {  // get_pt_within_unit_sphere(aa), hoisted (depends on aa and the pixel only)
