@@ -42,8 +42,12 @@ FLOP_PER_TEST = 20          # ~20 FLOP per ray-sphere test (FMA = 2
 PEAK_FP32_TFLOPS = 157.3    # MI355X_MICROARCH.md: peak FP32 vector (spec)
 PEAK_HBM_GBPS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 # algorithmic HBM bytes per pixel per launch: mode-1 pass 1 writes raw colour +
-# normal + depth (48 B); pass 2 unique minimum reads 48 B + writes pixel + image (32 B)
-BYTES_PER_PIXEL = {1: 48, 2: 80, 3: 64, 4: 32, 5: 32}
+# normal + depth (48 B); mode 2 also the image (64 B); modes 3/4 pixel + image (32 B).  The
+# post-process (pass 2) reads colour + normal + depth of its pixel (48 B; the 4 neighbours are
+# other pixels' bytes), 32 B (normal + depth) per history slot it examines and 16 B per slot
+# it accepts, and writes pixel + image (32 B): counted per launch from the kernel's counters.
+BYTES_PER_PIXEL = {1: 48, 3: 64, 4: 32, 5: 32}
+POST_BYTES_PIXEL, POST_BYTES_SLOT_READ, POST_BYTES_SLOT_ACCEPTED = 80, 32, 16
 
 
 def log(*a):
@@ -227,7 +231,7 @@ def main():
             "flop_per_launch": FLOP_PER_TEST * tests,
             "tests_per_launch": tests,
             "segments_per_sample": round(counts["segments"] / max(counts["samples"], 1), 4),
-            "lane_utilisation": round(counts["tests"] / max(counts["executed_lane_tests"], 1), 4),
+            "useful_test_ratio": round(counts["tests"] / max(counts["executed_lane_tests"], 1), 4),
             "hbm": {"achieved": round(hbm_alg, 2), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                     "frac": round(hbm_alg / PEAK_HBM_GBPS, 6),
                     "bytes_per_launch": BYTES_PER_PIXEL[dom] * band_px},
@@ -246,10 +250,13 @@ def main():
         if mode == 1:
             n_p, tot_p = kstats[2]
             pms = tot_p / max(n_p, 1)
-            pbw = BYTES_PER_PIXEL[2] * (r1 - r0) * W / (pms * 1e-3) / 1e9
+            post_bytes = (POST_BYTES_PIXEL * counts["post_pixels"] + POST_BYTES_SLOT_READ * counts["history_read"]
+                          + POST_BYTES_SLOT_ACCEPTED * counts["history_accepted"]) / ncount
+            pbw = post_bytes / (pms * 1e-3) / 1e9
             out["roofline_post"] = {"bound": "hbm", "achieved": round(pbw, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                                     "frac": round(pbw / PEAK_HBM_GBPS, 4), "kernel": "aop_postprocessing (post_kernel)",
-                                    "kernel_ms": round(pms, 4),
+                                    "kernel_ms": round(pms, 4), "bytes_per_launch": round(post_bytes),
+                                    "history_slots_read_per_pixel": round(counts["history_read"] / max(counts["post_pixels"], 1), 3),
                                     "traffic": traffic_data.get("2") if traffic_data else None}
         if world == 1 and not args.no_cpu_baseline:
             try:

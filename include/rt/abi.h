@@ -131,10 +131,11 @@ int rt_reset_stats(rt_ctx* ctx);
  * segments (one scene loop each), [2] shadow rays, [3] ray-shape tests = ([1] + [2]) *
  * int(mode.z) — the algorithmic-FLOP basis of the roofline (20 FLOP per ray-sphere test,
  * SURVEY.md §8d), [4] executed lane-tests = sum over wavefronts of 64 x the shapes their scene
- * loops tested (divergence and culling: [3]/[4] is the useful fraction). */
+ * loops tested (divergence and culling: [3]/[4] is the useful fraction); post-process:
+ * [5] filtered pixels, [6] history slots read, [7] history slots accepted. */
 int rt_enable_counters(rt_ctx* ctx, int on);
-/* Read the 5 totals (synchronises); reset != 0 zeroes them afterwards. */
-int rt_read_counters(rt_ctx* ctx, uint64_t out[5], int reset);
+/* Read the 8 totals (synchronises); reset != 0 zeroes them afterwards. */
+int rt_read_counters(rt_ctx* ctx, uint64_t out[8], int reset);
 /* Per-row segment + shadow-ray counts of this context's rows (R = row_end - row_begin
  * entries), collected while counters are on: the cost profile used to balance row strips
  * across GPUs. */

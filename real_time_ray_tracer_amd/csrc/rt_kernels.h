@@ -5,7 +5,7 @@
 namespace rt {
 
 constexpr int kMaxFrames = 16;
-constexpr int kCounters = 5;
+constexpr int kCounters = 8;
 constexpr int kCounterSlots = 256;  // per counter, summed by the host
 
 // Everything one program launch needs.  Passed by value as the kernel argument (lives in the
@@ -37,6 +37,7 @@ struct FrameParams {
   // optional work counters (nullptr in timed runs): [0] primary samples, [1] closest-hit
   // segments, [2] shadow rays, [3] ray-shape tests = (segments + shadow rays) * nobj,
   // [4] executed lane-tests = sum over waves of 64 x (shapes tested by the wave's scene loops);
+  // post-process: [5] filtered pixels, [6] history slots read, [7] history slots accepted;
   // each counter has kCounterSlots copies (index k * kCounterSlots + slot)
   unsigned long long* counters;
   // optional per-row closest-hit segment counts, indexed by (y - band_row0) (nullptr = off)

@@ -908,6 +908,8 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
 // neighbours read `raw` (slot f before filtering); right iff x+1<W, left iff x>0,
 // up iff y+1<H, down iff y>=2.  Output goes to out_pix (the shim swaps it into slot f).
 // ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, unsigned& visited, unsigned& accepted);
+
 __device__ __forceinline__ float nbr_weight(f3 n, float nd, float nb, float4 kn, float4 kd) {
   if (kn.w < 0.001f) return 1.0f;
   float normal_dot = dot(n, xyz(kn));
@@ -919,7 +921,22 @@ __device__ __forceinline__ float nbr_weight(f3 n, float nd, float nb, float4 kn,
 __global__ __launch_bounds__(kBlock) void post_kernel(FrameParams P) {
   int x, y;
   tile_xy(x, y, P.trace_row0);
-  if (x >= P.W || y >= P.trace_row0 + P.trace_rows) return;
+  const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
+  unsigned visited = 0, accepted = 0;
+  if (active) post_pixel(P, x, y, visited, accepted);
+  if (P.counters) {
+    unsigned n = wave_sum(active ? 1u : 0u), v = wave_sum(visited), a = wave_sum(accepted);
+    if ((threadIdx.x & 63) == 0) {
+      unsigned long long* c = P.counters + ((blockIdx.x * 4 + blockIdx.y * 4 * gridDim.x + (threadIdx.x >> 6)) &
+                                            (kCounterSlots - 1));
+      atomicAdd(&c[5 * kCounterSlots], (unsigned long long)n);
+      atomicAdd(&c[6 * kCounterSlots], (unsigned long long)v);
+      atomicAdd(&c[7 * kCounterSlots], (unsigned long long)a);
+    }
+  }
+}
+
+__device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, unsigned& visited, unsigned& accepted) {
   const int W = P.W, f = P.frame;
   const size_t off = (size_t)(y - P.band_row0) * W + x;
   float4 color = P.raw[off];
@@ -961,7 +978,9 @@ __global__ __launch_bounds__(kBlock) void post_kernel(FrameParams P) {
       float depth_diff = 1.0f - gclamp(fabsf(nd - hd.x), 0.0f, 1.0f);
       float bounces_diff = 1.0f - gclamp(fabsf(nb - hd.y) / 1.7f, 0.0f, 1.0f);
       float coeff = normal_dot * depth_diff * bounces_diff;
+      ++visited;
       if (!(coeff > 0.85f)) break;
+      ++accepted;
       float4 hp = P.hist_pix[cf][off];
       cs.x = cs.x + coeff * hp.x; cs.y = cs.y + coeff * hp.y;
       cs.z = cs.z + coeff * hp.z; cs.w = cs.w + coeff * hp.w;

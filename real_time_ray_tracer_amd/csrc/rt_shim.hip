@@ -580,7 +580,7 @@ int rt_enable_counters(rt_ctx* c, int on) {
   return RT_OK;
 }
 
-int rt_read_counters(rt_ctx* c, uint64_t out[5], int reset) {
+int rt_read_counters(rt_ctx* c, uint64_t out[8], int reset) {
   if (!c || !out) return RT_E_INVAL;
   if (!c->d_counters) {
     for (int k = 0; k < rt::kCounters; ++k) out[k] = 0;

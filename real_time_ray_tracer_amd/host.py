@@ -276,10 +276,11 @@ class Renderer:
         self._c(self._lib.rt_enable_counters(self.ctx, int(totals) | (2 if rows else 0)), "rt_enable_counters")
 
     def read_counters(self, reset: bool = True) -> dict:
-        out = (C.c_uint64 * 5)()
+        out = (C.c_uint64 * 8)()
         self._c(self._lib.rt_read_counters(self.ctx, out, int(reset)), "rt_read_counters")
         return {"samples": out[0], "segments": out[1], "shadow_rays": out[2], "tests": out[3],
-                "executed_lane_tests": out[4]}
+                "executed_lane_tests": out[4], "post_pixels": out[5], "history_read": out[6],
+                "history_accepted": out[7]}
 
     def read_row_counters(self, reset: bool = True) -> np.ndarray:
         out = np.zeros(self.R, np.uint64)

@@ -20,3 +20,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fe
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
   python3 bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> "$OUT/pmc_write.err"
 find "$OUT" -name "*.csv" | head -50
+python3 tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$CFG" "$OUT/pmc.json"
