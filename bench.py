@@ -111,6 +111,10 @@ def main():
     ap.add_argument("--no-balance", action="store_true", help="equal strips instead of cost-balanced")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--verify", action="store_true",
+                    help="rank 0 also renders every frame whole and checks the gathered frames bit for bit")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearsal of the N>1 path with ranks sharing GPUs, gather staged through host")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -122,10 +126,15 @@ def main():
     from real_time_ray_tracer_amd import Header, Renderer, aspect_for
     from real_time_ray_tracer_amd.dist import StripGather, StripPlan, balanced_bounds, equal_bounds
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    gpu = local_rank if args.backend == "nccl" else local_rank % torch.cuda.device_count()
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    cdev = dev if args.backend == "nccl" else torch.device("cpu")  # collective tensors
 
     W, H, S, spp, mode, desc = CONFIGS[args.config]
     header = Header.synthetic(S, spp, 1234 + CONFIG_INDEX[args.config], aspect_for(W, H))
@@ -134,7 +143,7 @@ def main():
     # ---- strip plan: cost-balanced from the kernels' per-row segment counts -----------------
     bounds = equal_bounds(H, world)
     if world > 1 and not args.no_balance:
-        probe = Renderer(W, H, S, spp, device=local_rank, rows=(bounds[rank], bounds[rank + 1]))
+        probe = Renderer(W, H, S, spp, device=gpu, rows=(bounds[rank], bounds[rank + 1]))
         probe.set_stream(stream.cuda_stream)
         probe.enable_counters(totals=False, rows=True)
         header.fill_rand_buffer(7000)
@@ -143,16 +152,35 @@ def main():
         probe.dispatch(mode, 0)
         mine = probe.read_row_counters().astype(np.float64)
         probe.close()
-        full = torch.zeros(H, dtype=torch.float64, device=dev)
-        full[bounds[rank]:bounds[rank + 1]] = torch.from_numpy(mine).to(dev)
+        full = torch.zeros(H, dtype=torch.float64, device=cdev)
+        full[bounds[rank]:bounds[rank + 1]] = torch.from_numpy(mine).to(cdev)
         dist.all_reduce(full)
         bounds = balanced_bounds(full.cpu().numpy(), world)
     plan = StripPlan(W, H, bounds)
     r0, r1 = plan.rows(rank)
-    rend = Renderer(W, H, S, spp, device=local_rank, rows=(r0, r1))
+    rend = Renderer(W, H, S, spp, device=gpu, rows=(r0, r1))
     rend.set_stream(stream.cuda_stream)
-    gather = StripGather(plan, rank, dev) if world > 1 else None
-    state = {"frame": 0}
+    gather = StripGather(plan, rank, dev, host_staging=args.backend == "gloo") if world > 1 else None
+    state = {"frame": 0, "ref_frame": 0, "mismatch": 0, "checked": 0}
+    ref = None
+    if args.verify and rank == 0:
+        ref = Renderer(W, H, S, spp, device=gpu)
+        ref.set_stream(stream.cuda_stream)
+
+    def verify(k: int):
+        # rank 0: the gathered frame of frame k must equal the whole-frame render, bit for bit
+        import torch as _t
+        ref.upload_header(header)
+        state["ref_frame"] = ref.dispatch(mode, state["ref_frame"])
+        if gather is None:
+            return
+        gather.finish()
+        got = gather.frame(k).cpu().numpy()[:H]
+        want = ref.image()
+        state["checked"] += 1
+        if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+            state["mismatch"] += 1
+        _t.cuda.synchronize()
 
     def step(k: int):
         if mode in (1, 2):
@@ -166,6 +194,8 @@ def main():
         state["frame"] = rend.dispatch(mode, state["frame"])
         if gather is not None:
             gather.gather(k)
+        if ref is not None:
+            verify(k)
 
     for k in range(args.warmup):
         step(k)
@@ -203,7 +233,7 @@ def main():
     counts = rend.read_counters(reset=True)
     rend.enable_counters(False)
 
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     elapsed = float(t_max.item())
@@ -247,6 +277,8 @@ def main():
                        "parallelism": f"{world} row strip(s), cost-balanced" + (", RCCL gather to rank 0" if world > 1 else "")},
             "roofline": roof,
         }
+        if args.verify:
+            out["verify"] = {"frames_checked": state["checked"], "mismatched": state["mismatch"]}
         if mode == 1:
             n_p, tot_p = kstats[2]
             pms = tot_p / max(n_p, 1)

@@ -73,18 +73,22 @@ class StripGather:
     (RCCL on GPUs, gloo on CPU).  Strips are padded to max_rows so one gather moves them all;
     with equal strips the gather lands directly in the frame tensor (no assembly copy)."""
 
-    def __init__(self, plan: StripPlan, rank: int, device, nbuf: int = 2, root: int = 0):
+    def __init__(self, plan: StripPlan, rank: int, device, nbuf: int = 2, root: int = 0, host_staging: bool = False):
+        """host_staging: gather through host copies (gloo rehearsal of the GPU path)."""
         import torch
 
         self.plan, self.rank, self.root, self.nbuf = plan, rank, root, nbuf
+        self.host_staging = host_staging
+        self.device = device
         R, W = plan.max_rows, plan.W
         self.equal = all(plan.bounds[i + 1] - plan.bounds[i] == R for i in range(plan.n))
         self.strips = [torch.zeros((R, W, 4), dtype=torch.float32, device=device) for _ in range(nbuf)]
         self.frames = []
         self.lists = []
+        fdev = "cpu" if host_staging else device
         if rank == root:
             for _ in range(nbuf):
-                frame = torch.zeros((plan.n * R, W, 4), dtype=torch.float32, device=device)
+                frame = torch.zeros((plan.n * R, W, 4), dtype=torch.float32, device=fdev)
                 self.frames.append(frame)
                 self.lists.append(list(frame.split(R, 0)))
         self.pending = [None] * nbuf
@@ -102,7 +106,8 @@ class StripGather:
 
         i = k % self.nbuf
         lst = self.lists[i] if self.rank == self.root else None
-        work = dist.gather(self.strips[i], gather_list=lst, dst=self.root, async_op=async_op)
+        src = self.strips[i].cpu() if self.host_staging else self.strips[i]
+        work = dist.gather(src, gather_list=lst, dst=self.root, async_op=async_op)
         if async_op:
             self.pending[i] = work
 
