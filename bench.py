@@ -138,13 +138,15 @@ def main():
 
     W, H, S, spp, mode, desc = CONFIGS[args.config]
     header = Header.synthetic(S, spp, 1234 + CONFIG_INDEX[args.config], aspect_for(W, H))
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated stream: the renderer, the gather and torch's copies are all ordered on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
 
     # ---- strip plan: cost-balanced from the kernels' per-row segment counts -----------------
     bounds = equal_bounds(H, world)
     if world > 1 and not args.no_balance:
         probe = Renderer(W, H, S, spp, device=gpu, rows=(bounds[rank], bounds[rank + 1]))
-        probe.set_stream(stream.cuda_stream)
+        probe.set_stream(stream)
         probe.enable_counters(totals=False, rows=True)
         header.fill_rand_buffer(7000)
         header.set_mode(0, S)
@@ -159,13 +161,13 @@ def main():
     plan = StripPlan(W, H, bounds)
     r0, r1 = plan.rows(rank)
     rend = Renderer(W, H, S, spp, device=gpu, rows=(r0, r1))
-    rend.set_stream(stream.cuda_stream)
+    rend.set_stream(stream)
     gather = StripGather(plan, rank, dev, host_staging=args.backend == "gloo") if world > 1 else None
     state = {"frame": 0, "ref_frame": 0, "mismatch": 0, "checked": 0}
     ref = None
     if args.verify and rank == 0:
         ref = Renderer(W, H, S, spp, device=gpu)
-        ref.set_stream(stream.cuda_stream)
+        ref.set_stream(stream)
 
     def verify(k: int):
         # rank 0: the gathered frame of frame k must equal the whole-frame render, bit for bit
@@ -173,13 +175,18 @@ def main():
         ref.upload_header(header)
         state["ref_frame"] = ref.dispatch(mode, state["ref_frame"])
         if gather is None:
-            return
-        gather.finish()
-        got = gather.frame(k).cpu().numpy()[:H]
+            got = rend.image()
+        else:
+            gather.finish()
+            got = gather.frame(k).cpu().numpy()[:H]
         want = ref.image()
         state["checked"] += 1
-        if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+        bad = np.any(got.view(np.uint32) != want.view(np.uint32), axis=2)
+        if bad.any():
             state["mismatch"] += 1
+            ys = np.nonzero(bad.any(axis=1))[0]
+            state.setdefault("diag", []).append({"frame": k, "pixels": int(bad.sum()), "rows": [int(ys.min()), int(ys.max())],
+                                                 "nrows": int(len(ys))})
         _t.cuda.synchronize()
 
     def step(k: int):
@@ -278,7 +285,8 @@ def main():
             "roofline": roof,
         }
         if args.verify:
-            out["verify"] = {"frames_checked": state["checked"], "mismatched": state["mismatch"]}
+            out["verify"] = {"frames_checked": state["checked"], "mismatched": state["mismatch"],
+                             "diag": state.get("diag", [])[:6]}
         if mode == 1:
             n_p, tot_p = kstats[2]
             pms = tot_p / max(n_p, 1)

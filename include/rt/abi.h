@@ -79,9 +79,11 @@ typedef struct {
  * resident header, g-buffer ring (zeroed like the value-initialised ssbo_CPUMEM) and image. */
 int rt_create(int device, const rt_config* cfg, rt_ctx** out);
 int rt_destroy(rt_ctx* ctx);
-/* Order all of the context's work on an external HIP stream (hipStream_t); NULL restores the
- * context's own stream. */
+/* Order all of the context's work on an external HIP stream (hipStream_t).  NULL is the
+ * device's legacy NULL stream (e.g. torch's default stream), not "no stream". */
 int rt_set_stream(rt_ctx* ctx, void* hip_stream);
+/* Go back to the context's own (non-blocking) stream. */
+int rt_use_own_stream(rt_ctx* ctx);
 void* rt_get_stream(rt_ctx* ctx);
 int rt_synchronize(rt_ctx* ctx);
 int rt_last_hip_error(rt_ctx* ctx);

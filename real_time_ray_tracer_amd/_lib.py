@@ -41,6 +41,7 @@ SIGNATURES = {
     "rt_create": (C.c_int, [C.c_int, C.POINTER(rt_config), C.POINTER(_ctx)]),
     "rt_destroy": (C.c_int, [_ctx]),
     "rt_set_stream": (C.c_int, [_ctx, _vp]),
+    "rt_use_own_stream": (C.c_int, [_ctx]),
     "rt_get_stream": (_vp, [_ctx]),
     "rt_synchronize": (C.c_int, [_ctx]),
     "rt_last_hip_error": (C.c_int, [_ctx]),

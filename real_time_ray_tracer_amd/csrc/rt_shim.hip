@@ -362,8 +362,17 @@ int rt_destroy(rt_ctx* c) {
 
 int rt_set_stream(rt_ctx* c, void* s) {
   if (!c) return RT_E_INVAL;
+  RT_HIP(c, hipSetDevice(c->device));
   RT_HIP(c, hipStreamSynchronize(c->stream));
-  c->stream = s ? (hipStream_t)s : c->own_stream;
+  c->stream = (hipStream_t)s;  // NULL = the legacy NULL stream
+  return RT_OK;
+}
+
+int rt_use_own_stream(rt_ctx* c) {
+  if (!c) return RT_E_INVAL;
+  RT_HIP(c, hipSetDevice(c->device));
+  RT_HIP(c, hipStreamSynchronize(c->stream));
+  c->stream = c->own_stream;
   return RT_OK;
 }
 

@@ -203,9 +203,13 @@ class Renderer:
 
     # streams
     def set_stream(self, stream):
-        """stream: a torch.cuda.Stream, an int hipStream_t, or None (own stream)."""
-        ptr = getattr(stream, "cuda_stream", stream)
-        self._c(self._lib.rt_set_stream(self.ctx, C.c_void_p(ptr) if ptr else None), "rt_set_stream")
+        """Order the context's work on `stream`: a torch.cuda.Stream or an int hipStream_t
+        (0 = the NULL stream, which is torch's default stream); None = the context's own stream."""
+        if stream is None:
+            self._c(self._lib.rt_use_own_stream(self.ctx), "rt_use_own_stream")
+            return
+        ptr = int(getattr(stream, "cuda_stream", stream))
+        self._c(self._lib.rt_set_stream(self.ctx, C.c_void_p(ptr)), "rt_set_stream")
 
     def synchronize(self):
         self._c(self._lib.rt_synchronize(self.ctx), "rt_synchronize")
