@@ -170,9 +170,9 @@ __device__ __forceinline__ void sphere_candidate(f3 pos, f3 dir, float4 g, int i
   }
 }
 
-// Variant of closest_hit for the A/B experiment: min-t update inside the hit branch and the
-// geometry of 4 spheres fetched before any of them is tested (V = 1: from LDS; V = 2: the
-// same table in global memory read with wave-uniform scalar loads).  Bit-identical results.
+// All-sphere closest hit with the min-t update inside the hit branch and the geometry of 4
+// spheres fetched before any of them is tested (V = 2: global table read with wave-uniform
+// scalar loads; V = 0: closest_hit).  Bit-identical to closest_hit.
 template <bool ALLSPH, int V>
 __device__ __forceinline__ int closest_hit_v(const float4* __restrict__ geo, const float4* __restrict__ geo2,
                                              int nobj, f3 pos, f3 dir, float thr, float& t_out) {

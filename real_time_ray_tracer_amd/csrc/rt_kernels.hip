@@ -344,64 +344,13 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4*
 }
 
 // ---------------------------------------------------------------------------------------
-// modes 1/2 pass 1, pooled (all-sphere scenes).  One wave per workgroup owns a pool of
-// kPool pixel-samples: TP = kPool/spp consecutive pixels of the traced rows x spp samples.
-//  * path regeneration: a lane whose path ends takes the next sample of the pool, so the
-//    bounce rounds keep (nearly) every lane busy instead of waiting for the wave's longest
-//    path;
-//  * primary-ray culling: every primary ray starts at the camera and passes through the
-//    pool's pixel rectangle (jitter < 0.0834 px), so a sphere whose line distance from all
-//    rays of that frustum cone exceeds its radius by a float-error margin has a computed
-//    discriminant < 0 for every lane (-1 in the reference, never accepted) and is skipped.
-//    Survivors are tested in increasing index order, so ties resolve as in the reference.
-// Per-sample results go to LDS and are combined in sample order as in ao_kernel.
+// Primary-ray cone culling (used by ao_batch_kernel).  Every primary ray starts at the camera
+// and passes through the pool's pixel rectangle (jitter < 0.0834 px), so one cone bounds
+// them.  A sphere whose line distance from every ray of the cone exceeds its radius by a
+// float-error margin has a computed discriminant < 0 for every lane (-1 in the reference,
+// never accepted) and is skipped.
 // ---------------------------------------------------------------------------------------
 constexpr int kPool = 256;
-
-// Conservative cone around the primary rays of pixel rect [xmin,xmax] x [ymin,ymax].
-__device__ inline void pool_cone(const FrameParams& P, int xmin, int xmax, int ymin, int ymax, double a[3],
-                                 double& theta) {
-  const double hps[2] = {((double)xmin - 0.1) / P.W, ((double)xmax + 0.1) / P.W};
-  const double vps[2] = {((double)ymin - 0.1) / P.H, ((double)ymax + 0.1) / P.H};
-  double d[4][3], s[3] = {0.0, 0.0, 0.0};
-  for (int k = 0; k < 4; ++k) {
-    double hp = hps[k & 1], vp = vps[k >> 1];
-    double x = (double)P.lx + hp * P.hx + vp * P.vx;
-    double y = (double)P.ly + hp * P.hy + vp * P.vy;
-    double z = (double)P.lz + hp * P.hz + vp * P.vz;
-    double l = sqrt(x * x + y * y + z * z);
-    d[k][0] = x / l; d[k][1] = y / l; d[k][2] = z / l;
-    s[0] += d[k][0]; s[1] += d[k][1]; s[2] += d[k][2];
-  }
-  double l = sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
-  a[0] = s[0] / l; a[1] = s[1] / l; a[2] = s[2] / l;
-  double th = 0.0;
-  for (int k = 0; k < 4; ++k) {
-    double c = a[0] * d[k][0] + a[1] * d[k][1] + a[2] * d[k][2];
-    c = c > 1.0 ? 1.0 : (c < -1.0 ? -1.0 : c);
-    th = fmax(th, acos(c));
-  }
-  theta = th + 1e-5;  // + float error of the lanes' directions (~1e-6 rad)
-}
-
-// True when every ray from the camera inside the cone misses sphere g with a margin that
-// covers the float error of the discriminant: dist^2 sin^2(psi) > r^2 + 1e-5 (dist^2 + r^2)
-// for every angle psi between a ray and the centre direction (the computed del then stays
-// < 0; its error is below 2e-6 dist^2).
-__device__ inline bool cone_misses(const double a[3], double theta, float4 g, float cx, float cy, float cz) {
-  double Lx = (double)g.x - cx, Ly = (double)g.y - cy, Lz = (double)g.z - cz;
-  double d2 = Lx * Lx + Ly * Ly + Lz * Lz, r2 = (double)g.w * g.w;
-  if (!(d2 > r2 * 1.001 + 1e-6)) return false;  // camera inside / on the sphere: keep
-  double dist = sqrt(d2);
-  double c = (a[0] * Lx + a[1] * Ly + a[2] * Lz) / dist;
-  c = c > 1.0 ? 1.0 : (c < -1.0 ? -1.0 : c);
-  double phi = acos(c);
-  double lo = phi - theta;
-  if (!(lo > 1e-5)) return false;
-  double hi = fmin(3.141592653589793, phi + theta);
-  double sm = fmin(sin(lo), sin(hi));
-  return d2 * sm * sm > r2 + 1e-5 * (d2 + r2);
-}
 
 // Float form of the same cull (no trig): cone axis a, cos/sin of the half-angle; a sphere
 // with inflated radius r_eff (r_eff^2 = r^2 + 1e-5 (d^2 + r^2)) lies outside the forward and
@@ -447,212 +396,10 @@ __device__ inline bool cone_misses_f(const ConeF& c, float4 g, float cx, float c
   return fabsf(cphi) < K;
 }
 
-template <int MINW>
-__global__ __launch_bounds__(64, MINW) void ao_pool_kernel(FrameParams P, const float4* __restrict__ geo) {
-  extern __shared__ float4 lds[];
-  const int spp = P.spp, W = P.W, D = P.D, nobj = P.nobj;
-  const int TP = kPool / spp > 0 ? kPool / spp : 1;
-  const int lane = threadIdx.x;
-  float4* samp = lds;                      // [TP*spp] (r, g, b, stop value or -1)
-  float4* prec = lds + TP * spp;           // [TP] first-segment (normal, t) of sample 0
-  int* pkind = (int*)(prec + TP);          // [TP]
-  unsigned long long* cmask = (unsigned long long*)(pkind + ((TP + 1) & ~1));  // [ceil(nobj/64)]
-  const float4* col = P.shapes + 2 * P.S;
-  const float4* aux = P.shapes + 3 * P.S;
-
-  const long long npix = (long long)P.trace_rows * W;
-  const long long p0 = (long long)blockIdx.x * TP;
-  const int np = (int)(npix - p0 < TP ? npix - p0 : TP);
-  const int total = np * spp;
-
-  // ---- frustum cull of the primary rays -------------------------------------------------
-  const int yf = P.trace_row0 + (int)(p0 / W), xf = (int)(p0 % W);
-  const int yl = P.trace_row0 + (int)((p0 + np - 1) / W), xl = (int)((p0 + np - 1) % W);
-  double ca[3], th;
-  pool_cone(P, yf == yl ? xf : 0, yf == yl ? xl : W - 1, yf, yl, ca, th);
-  const int nwords = (nobj + 63) >> 6;
-  int ncull = 0;
-  for (int w = 0; w < nwords; ++w) {
-    int i = (w << 6) + lane;
-    bool keep = i < nobj && !cone_misses(ca, th, geo[i], P.cx, P.cy, P.cz);
-    unsigned long long m = __ballot(keep);
-    ncull += __popcll(m);
-    if (lane == 0) cmask[w] = m;
-  }
-  __syncthreads();
-
-  const f3 cam = mk(P.cx, P.cy, P.cz);
-  const float4* rbuf = P.rb;
-  int next = 0;            // wave-uniform: next pool sample
-  bool has = false;        // this lane holds a live path
-  int item = 0, depth = 0;
-  f3 pos = cam, dir = cam, hemi = cam;
-  float rr = 1.0f, rg = 1.0f, rb = 1.0f;
-  unsigned nseg = 0, sseg = 0;
-  unsigned long long exec_tests = 0;  // wave-uniform: shapes tested by the wave's loops
-
-  // One segment's bookkeeping (ao_compute.glsl:196-260 + ambient_occlusion 273-281).
-  auto segment = [&](int ind, float t) {
-    const int lp = item / spp, aa = item - lp * spp;
-    const bool first = depth == D;
-    ++nseg;
-    ++sseg;
-    float stopv = -2.0f;  // -2: path continues
-    if (ind != -1) {
-      float4 att = col[ind];
-      float4 ax = aux[ind];
-      if (ax.x > 0.9f) {
-        rr = rr * att.x; rg = rg * att.y; rb = rb * att.z;
-        stopv = (float)(D - depth);
-        if (aa == 0 && first) pkind[lp] = PRIM_EMISSIVE;
-      } else {
-        f3 curr = cam + t * dir;  // sic: camera origin (ao_compute.glsl:210)
-        f3 nn = normalize(curr - xyz(geo[ind]));
-        if (aa == 0 && first) {
-          pkind[lp] = PRIM_HIT;
-          prec[lp] = make_float4(nn.x, nn.y, nn.z, t);
-        }
-        rr = rr * att.x; rg = rg * att.y; rb = rb * att.z;
-        pos = curr;
-        float reflect = ax.y;
-        if (reflect > 0.999f) {
-          dir = normalize(hemi + nn);
-        } else {
-          float dn = dot(dir, nn);
-          f3 R = normalize(mk(dir.x - 2.0f * (dn * nn.x), dir.y - 2.0f * (dn * nn.y), dir.z - 2.0f * (dn * nn.z)));
-          dir = normalize(R + reflect * hemi);
-        }
-        depth -= 1;
-        if (depth == 0) stopv = -1.0f;  // RECURSION_DEPTH non-emissive hits: no stop write
-      }
-    } else {
-      if (aa == 0 && first) pkind[lp] = PRIM_MISS;
-      rr = rr * P.bg.x; rg = rg * P.bg.y; rb = rb * P.bg.z;
-      stopv = (float)(D - depth);
-    }
-    if (stopv != -2.0f) {
-      samp[item] = make_float4(rr, rg, rb, stopv);
-      if (P.row_counters) {
-        int y = P.trace_row0 + (int)((p0 + lp) / W);
-        atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)sseg);
-      }
-      has = false;
-    }
-  };
-
-  for (;;) {
-    // ---- refill idle lanes with new samples and trace their primary rays (culled set) ----
-    for (;;) {
-      unsigned long long need = __ballot(!has);
-      if (need == 0 || next >= total) break;
-      int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
-      bool got = !has && next + rank < total;
-      int avail = total - next, want = __popcll(need);
-      if (got) item = next + rank;
-      next += want < avail ? want : avail;
-      exec_tests += (unsigned long long)ncull;
-      if (got) {
-        const int lp = item / spp, aa = item - lp * spp;
-        const long long pix = p0 + lp;
-        const int x = (int)(pix % W), y = P.trace_row0 + (int)(pix / W);
-        const float px = (float)x, py = (float)y;
-        float hp, vp;
-        if (aa == 0) {
-          hp = px / (float)W;
-          vp = py / (float)P.H;
-        } else {  // ao_compute.glsl:310-323
-          float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
-          float u = grandom(((s.x + px * f.z) - px) + f.x, ((f.y + py * s.w) - py) + s.y);
-          float w = grandom(s.z * px - (f.x * px) * f.z, f.w * py - (s.y * py) * s.w);
-          normalize2(u, w);
-          hp = (px + (u / 6.0f - 0.08333f)) / (float)W;
-          vp = (py + (w / 6.0f - 0.08333f)) / (float)P.H;
-        }
-        dir = primary_dir(P, hp, vp);
-        {  // get_pt_within_unit_sphere(aa), hoisted (depends on aa and the pixel only)
-          float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
-          float a = grandom(f.x + px * s.z, f.y + py * s.w);
-          float b = grandom(f.z - px * s.z, f.w - py * s.w);
-          float e = grandom(s.x * px + s.z, s.y * py + s.w);
-          hemi = normalize(mk(a * 2.0f - 1.0f, b * 2.0f - 1.0f, e * 2.0f - 1.0f));
-        }
-        pos = cam;
-        rr = rg = rb = 1.0f;
-        depth = D;
-        sseg = 0;
-        has = true;
-        float t = -1.0f;
-        int ind = -1;
-        for (int w = 0; w < nwords; ++w) {
-          unsigned long long m = cmask[w];
-          m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
-              (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
-          while (m) {
-            int i = (w << 6) + __builtin_ctzll(m);
-            m &= m - 1;
-            sphere_candidate(pos, dir, geo[i], i, 0.0001f, t, ind);
-          }
-        }
-        segment(ind, t);
-      }
-    }
-    if (__ballot(has) == 0) break;
-    // ---- one bounce segment for every live path, against every sphere ------------------
-    exec_tests += (unsigned long long)nobj;
-    if (has) {
-      float t;
-      int ind = closest_hit_v<true, 2>(geo, geo, nobj, pos, dir, 0.0001f, t);
-      segment(ind, t);
-    }
-  }
-
-  if (P.counters) {
-    unsigned sg = wave_sum(nseg);
-    if (lane == 0) {
-      unsigned long long* c = P.counters + (blockIdx.x & (kCounterSlots - 1));
-      atomicAdd(&c[0 * kCounterSlots], (unsigned long long)total);
-      atomicAdd(&c[1 * kCounterSlots], (unsigned long long)sg);
-      atomicAdd(&c[3 * kCounterSlots], (unsigned long long)sg * (unsigned long long)nobj);
-      atomicAdd(&c[4 * kCounterSlots], 64ull * exec_tests);
-    }
-  }
-  __syncthreads();
-
-  // ---- sample combine in aa order (ao_compute.glsl:303-339) ----------------------------
-  for (int lp = lane; lp < np; lp += 64) {
-    const long long pix = p0 + lp;
-    const int x = (int)(pix % W), y = P.trace_row0 + (int)(pix / W);
-    float sr = 0.0f, sg = 0.0f, sb = 0.0f, ystop = -1.0f;
-    const float4* ps = samp + lp * spp;
-    for (int k = 0; k < spp; ++k) {
-      float4 q = ps[k];
-      sr = sr + q.x; sg = sg + q.y; sb = sb + q.z;
-      if (q.w >= 0.0f) ystop = q.w;
-    }
-    const float fa = (float)spp;
-    const size_t off = (size_t)(y - P.band_row0) * W + x;
-    const int kind = pkind[lp];
-    float4 d;
-    if (kind == PRIM_HIT) {
-      float4 r0 = prec[lp];
-      d = make_float4(r0.w, 0.0f, 0.0f, 1.0f);
-      P.nrm[off] = make_float4(r0.x, r0.y, r0.z, 1.0f);
-    } else if (kind == PRIM_MISS) {
-      d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      P.nrm[off] = d;
-    } else {
-      d = P.dep[off];
-    }
-    if (ystop >= 0.0f) d.y = ystop;
-    d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
-    P.dep[off] = d;
-    store_color(P, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
-  }
-}
-
 // ---------------------------------------------------------------------------------------
-// Pooled AO, batch-prepared (variant 6).  As ao_pool_kernel, but new samples are prepared 64
-// at a time with the whole wave active: primary direction + hemisphere vector + primary hit
+// Pooled AO (all-sphere scenes).  One wave per workgroup owns a pool of kPool pixel-samples
+// (TP = kPool/spp consecutive pixels x spp samples).  New samples are prepared 64 at a time
+// with the whole wave active: primary direction + hemisphere vector + primary hit
 // over the culled set + first-hit shading.  Samples whose path ended at the primary hit are
 // final at once; the live post-primary states are kept in the lanes that prepared them and
 // handed to idle lanes by ds_bpermute whenever lanes run out of work.  Bounce rounds then
@@ -1034,25 +781,14 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
     // is the pooled, batch-prepared kernel (7) for all-sphere scenes.
     const char* ev = getenv("RTRT_AO_VARIANT");
     const int variant = ev ? atoi(ev) : 7;
-    if (all_spheres && variant >= 3) {
+    if (all_spheres && variant == 7) {
       const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
       const long long pools = (npix + TP - 1) / TP;
       const size_t psh = (size_t)TP * p.spp * sizeof(float4) + (size_t)TP * sizeof(float4) +
-                         (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 1) * 8;
-      if (variant == 6)
-        hipLaunchKernelGGL(ao_batch_kernel<1>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
-      else if (variant == 7)
-        hipLaunchKernelGGL(ao_batch_kernel<6>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
-      else if (variant == 4)
-        hipLaunchKernelGGL(ao_pool_kernel<8>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
-      else if (variant == 5)
-        hipLaunchKernelGGL(ao_pool_kernel<6>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
-      else
-        hipLaunchKernelGGL(ao_pool_kernel<1>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+                         (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8;
+      hipLaunchKernelGGL(ao_batch_kernel<6>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
     } else if (!all_spheres)
       hipLaunchKernelGGL((ao_kernel<false, 0>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
-    else if (variant == 1)
-      hipLaunchKernelGGL((ao_kernel<true, 1>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
     else if (variant == 2)
       hipLaunchKernelGGL((ao_kernel<true, 2>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
     else

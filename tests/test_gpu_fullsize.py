@@ -1,0 +1,85 @@
+"""Parity at BASELINE.json's full sizes: the GPU renders the whole frame; the CPU oracle
+re-executes a band of rows (plus the 1-row halo the post-process needs) on the same inputs
+and frame sequence; the band must agree (normals/depth bit for bit, pixels within 1e-4).
+Plus size-independent properties of the whole frame (finite, non-negative, alpha 0)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from bench import CONFIG_INDEX, CONFIGS
+from conftest import assert_bitwise, assert_close
+from real_time_ray_tracer_amd import Header, Renderer, aspect_for
+
+pytestmark = pytest.mark.gpu
+
+
+def band_oracle(h0, W, H, mode, frames, y0, y1):
+    """Oracle over rows [y0, y1) with a 1-row halo band, same frame sequence as the GPU."""
+    gy0, gy1 = max(0, y0 - 1), min(H, y1 + 1)
+    gh = gy1 - gy0
+    d = oracle.dims(W, H, h0.S, h0.AA, gy0=gy0, gh=gh)
+    buf = np.zeros(h0.data.size + 3 * 8 * W * gh * 4, np.float32)
+    img = np.zeros((gh, W, 4), np.float32)
+    progs = {1: [oracle.AOP_COMPUTE, oracle.AOP_POSTPROCESSING], 2: [oracle.AO_COMPUTE],
+             3: [oracle.P_COMPUTE], 4: [oracle.H_COMPUTE]}[mode]
+    f = 0
+    for k in range(frames):
+        h = h0.copy()
+        if mode in (1, 2):
+            h.fill_rand_buffer(7000 + k)
+        h.set_mode(f, h.num_objects)
+        buf[:h.data.size] = h.data
+        for p in progs:
+            lo, hi = (y0, y1) if p in (oracle.AOP_POSTPROCESSING, oracle.P_COMPUTE, oracle.H_COMPUTE) else (gy0, gy1)
+            oracle.run_program(buf, d, p, f, img, lo, hi, nthreads=os.cpu_count() or 1)
+        f = (f + 1) % 8
+    o = h0.data.size
+    n = 8 * W * gh * 4
+    ring = [buf[o + i * n:o + (i + 1) * n].reshape(8, W, gh, 4) for i in range(3)]
+    sl = slice(y0 - gy0, y1 - gy0)
+    return img[sl], [r[:, :, sl] for r in ring]
+
+
+@pytest.mark.parametrize("cfg,frames,rows", [("b", 1, (500, 503)), ("d", 2, (1000, 1003)), ("c", 2, (700, 702)),
+                                             ("e", 1, (2000, 2001))])
+def test_full_size_band_parity(cfg, frames, rows):
+    W, H, S, spp, mode, _ = CONFIGS[cfg]
+    h0 = Header.synthetic(S, spp, 1234 + CONFIG_INDEX[cfg], aspect_for(W, H))
+    r = Renderer(W, H, S, spp)
+    f = 0
+    for k in range(frames):
+        h = h0.copy()
+        if mode in (1, 2):
+            h.fill_rand_buffer(7000 + k)
+        h.set_mode(f, S)
+        r.upload_header(h)
+        f = r.dispatch(mode, f)
+    img = r.image()
+    # size-independent properties of the whole frame
+    assert np.isfinite(img).all()
+    assert (img[..., :3] >= 0).all() and (img[..., 3] == 0).all()
+    y0, y1 = rows
+    bimg, (bp, bn, bd) = band_oracle(h0, W, H, mode, frames, y0, y1)
+    assert_close(img[y0:y1], bimg, f"config {cfg} image rows {rows}")
+    if mode in (1, 2):
+        g = r.download(True, True, True, False)
+        assert_bitwise(g.depth[:frames, :, y0:y1], bd[:frames], f"config {cfg} depth")
+        assert_bitwise(g.normals[:frames, :, y0:y1], bn[:frames], f"config {cfg} normals")
+        assert_close(g.pixels[:frames, :, y0:y1], bp[:frames], f"config {cfg} pixels")
+    r.close()
+
+
+@pytest.mark.parametrize("variant", ["0", "2"])
+def test_fallback_ao_kernels_match_oracle(variant, monkeypatch):
+    """The simple lane-per-sample AO kernels (used for scenes with planes, or forced) agree too."""
+    from test_gpu_parity import make_header, run_both
+
+    monkeypatch.setenv("RTRT_AO_VARIANT", variant)
+    W, H = 48, 32
+    for scene in ("syn16", "s6"):
+        h = make_header(scene, W, H, 4)
+        g, s, img = run_both(h, W, H, 1, 3)
+        assert_close(g.image, img, f"variant {variant} {scene}")
+        assert_bitwise(g.depth, s.depth, f"variant {variant} {scene} depth")
