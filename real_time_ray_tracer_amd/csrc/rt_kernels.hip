@@ -405,7 +405,7 @@ __device__ inline bool cone_misses_f(const ConeF& c, float4 g, float cx, float c
 // handed to idle lanes by ds_bpermute whenever lanes run out of work.  Bounce rounds then
 // run with (nearly) all lanes live, and no per-sample setup runs at partial utilisation.
 // ---------------------------------------------------------------------------------------
-template <int MINW>
+template <int MINW, bool LAZY = true>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   extern __shared__ float4 lds[];
   const int spp = P.spp, W = P.W, D = P.D, nobj = P.nobj;
@@ -440,6 +440,35 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     }
   }
   __syncthreads();
+
+  if (LAZY && ncull == 0) {
+    // Empty frustum: every primary ray of the pool provably misses every sphere, so each
+    // sample is "miss at the first segment": colour 1*background, depth.y = 0, zero g-buffer.
+    // Same float sequence as the general path (sum of spp background values, then / spp).
+    const float fa = (float)spp;
+    float sr = 0.0f, sg = 0.0f, sb = 0.0f;
+    for (int k = 0; k < spp; ++k) {
+      sr = sr + 1.0f * P.bg.x; sg = sg + 1.0f * P.bg.y; sb = sb + 1.0f * P.bg.z;
+    }
+    const float4 col = gamma_out(sr / fa, sg / fa, sb / fa);
+    const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int lp = lane; lp < np; lp += 64) {
+      const long long pix = p0 + lp;
+      const int x = (int)(pix % W), y = P.trace_row0 + (int)(pix / W);
+      const size_t off = (size_t)(y - P.band_row0) * W + x;
+      P.nrm[off] = z;
+      P.dep[off] = z;  // (0, 0, 0, 0) / AA
+      store_color(P, x, y, col);
+      if (P.row_counters) atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)spp);
+    }
+    if (P.counters && lane == 0) {
+      unsigned long long* c = P.counters + (blockIdx.x & (kCounterSlots - 1));
+      atomicAdd(&c[0 * kCounterSlots], (unsigned long long)total);
+      atomicAdd(&c[1 * kCounterSlots], (unsigned long long)total);
+      atomicAdd(&c[3 * kCounterSlots], (unsigned long long)total * (unsigned long long)nobj);
+    }
+    return;
+  }
 
   const f3 cam = mk(P.cx, P.cy, P.cz);
   const float4* rbuf = P.rb;
@@ -531,13 +560,17 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         vp = (py + (w / 6.0f - 0.08333f)) / (float)P.H;
       }
       bdir = primary_dir(P, hp, vp);
-      {  // get_pt_within_unit_sphere(aa), hoisted (depends on aa and the pixel only)
+      // get_pt_within_unit_sphere(aa), hoisted: it depends on aa and the pixel only, so it is
+      // computed once per sample — after the primary hit when LAZY (only a non-emissive hit
+      // uses it)
+      auto hemisphere = [&]() {
         float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
         float a = grandom(f.x + px * s.z, f.y + py * s.w);
         float b = grandom(f.z - px * s.z, f.w - py * s.w);
         float e = grandom(s.x * px + s.z, s.y * py + s.w);
-        bhemi = normalize(mk(a * 2.0f - 1.0f, b * 2.0f - 1.0f, e * 2.0f - 1.0f));
-      }
+        return normalize(mk(a * 2.0f - 1.0f, b * 2.0f - 1.0f, e * 2.0f - 1.0f));
+      };
+      if (!LAZY) bhemi = hemisphere();
       bpos = cam;
       br = bg = bb = 1.0f;
       float t = -1.0f;
@@ -553,6 +586,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         }
       }
       ++nseg;
+      if (LAZY && ind != -1 && !(aux[ind].x > 0.9f)) bhemi = hemisphere();
       live = shade(ind, t, bpos, bdir, bhemi, br, bg, bb, D, bitem, true);
     }
     unsigned long long lm = __ballot(live);
@@ -787,6 +821,12 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
       const size_t psh = (size_t)TP * p.spp * sizeof(float4) + (size_t)TP * sizeof(float4) +
                          (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8;
       hipLaunchKernelGGL(ao_batch_kernel<6>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+    } else if (all_spheres && variant == 11) {  // same without the lazy shortcuts (A/B)
+      const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
+      const long long pools = (npix + TP - 1) / TP;
+      const size_t psh = (size_t)TP * p.spp * sizeof(float4) + (size_t)TP * sizeof(float4) +
+                         (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8;
+      hipLaunchKernelGGL((ao_batch_kernel<6, false>), dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
     } else if (!all_spheres)
       hipLaunchKernelGGL((ao_kernel<false, 0>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
     else if (variant == 2)
