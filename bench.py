@@ -124,7 +124,8 @@ def main():
     import torch.distributed as dist
 
     from real_time_ray_tracer_amd import Header, Renderer, aspect_for
-    from real_time_ray_tracer_amd.dist import StripGather, StripPlan, balanced_bounds, equal_bounds
+    from real_time_ray_tracer_amd.dist import (StripGather, StripPlan, balanced_bounds, calibrate_row_cost, equal_bounds,
+                                               imbalance)
 
     gpu = local_rank if args.backend == "nccl" else local_rank % torch.cuda.device_count()
     torch.cuda.set_device(gpu)
@@ -142,22 +143,54 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
 
-    # ---- strip plan: cost-balanced from the kernels' per-row segment counts -----------------
+    # ---- strip plan: cost-balanced from the kernels' per-row work counters, then calibrated
+    # against each strip's measured kernel time (two passes) ------------------------------------
     bounds = equal_bounds(H, world)
+    balance_info = None
     if world > 1 and not args.no_balance:
-        probe = Renderer(W, H, S, spp, device=gpu, rows=(bounds[rank], bounds[rank + 1]))
-        probe.set_stream(stream)
-        probe.enable_counters(totals=False, rows=True)
-        header.fill_rand_buffer(7000)
-        header.set_mode(0, S)
-        probe.upload_header(header)
-        probe.dispatch(mode, 0)
-        mine = probe.read_row_counters().astype(np.float64)
-        probe.close()
+        def strip_run(bnd, frames, counters):
+            r = Renderer(W, H, S, spp, device=gpu, rows=(bnd[rank], bnd[rank + 1]))
+            r.set_stream(stream)
+            if counters:
+                r.enable_counters(totals=False, rows=True)
+            f = 0
+            for k in range(frames):
+                header.fill_rand_buffer(7000 + k) if mode in (1, 2) else header.moving_light(False)
+                header.set_mode(f, S)
+                r.upload_header(header)
+                if k == frames - 2 and not counters:
+                    r.enable_timing(True)
+                    r.reset_stats()
+                f = r.dispatch(mode, f)
+            out = r.read_row_counters().astype(np.float64) if counters else None
+            ms = 0.0
+            if not counters:
+                for p in {1: [1, 2], 2: [3], 3: [4], 4: [5]}[mode]:
+                    n_l, tot = r.kernel_stats(p)
+                    ms += tot / max(n_l, 1)
+            r.close()
+            return out, ms
+
+        mine, _ = strip_run(bounds, 1, True)
         full = torch.zeros(H, dtype=torch.float64, device=cdev)
         full[bounds[rank]:bounds[rank + 1]] = torch.from_numpy(mine).to(cdev)
         dist.all_reduce(full)
-        bounds = balanced_bounds(full.cpu().numpy(), world)
+        row_cost = full.cpu().numpy()
+        bounds = balanced_bounds(row_cost, world)
+        # calibration: time each strip (kernels only), rescale the profile, re-balance; twice
+        t_model = None
+        for _ in range(2):
+            _, ms = strip_run(bounds, 4 if mode in (1, 2) else 2, False)
+            tt = torch.zeros(world, dtype=torch.float64, device=cdev)
+            tt[rank] = ms
+            dist.all_reduce(tt)
+            t1 = tt.cpu().tolist()
+            if t_model is None:
+                t_model = (list(bounds), t1)
+            row_cost = calibrate_row_cost(bounds, row_cost, t1)
+            bounds = balanced_bounds(row_cost, world)
+        balance_info = {"model_bounds": t_model[0], "model_strip_ms": [round(t, 4) for t in t_model[1]],
+                        "model_imbalance": round(imbalance(t_model[1]), 4)}
     plan = StripPlan(W, H, bounds)
     r0, r1 = plan.rows(rank)
     rend = Renderer(W, H, S, spp, device=gpu, rows=(r0, r1))
@@ -241,8 +274,11 @@ def main():
     rend.enable_counters(False)
 
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    strip_ms = torch.zeros(world, dtype=torch.float64, device=cdev)
+    strip_ms[rank] = sum(tot / max(n_l, 1) for n_l, tot in kstats.values())
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(strip_ms)
     elapsed = float(t_max.item())
 
     if rank == 0:
@@ -284,6 +320,10 @@ def main():
                        "parallelism": f"{world} row strip(s), cost-balanced" + (", RCCL gather to rank 0" if world > 1 else "")},
             "roofline": roof,
         }
+        if balance_info is not None:
+            sm = strip_ms.cpu().tolist()
+            balance_info.update({"strip_ms": [round(t, 4) for t in sm], "imbalance": round(imbalance(sm), 4)})
+            out["config"]["balance"] = balance_info
         if args.verify:
             out["verify"] = {"frames_checked": state["checked"], "mismatched": state["mismatch"],
                              "diag": state.get("diag", [])[:6]}

@@ -138,9 +138,10 @@ int rt_reset_stats(rt_ctx* ctx);
 int rt_enable_counters(rt_ctx* ctx, int on);
 /* Read the 8 totals (synchronises); reset != 0 zeroes them afterwards. */
 int rt_read_counters(rt_ctx* ctx, uint64_t out[8], int reset);
-/* Per-row segment + shadow-ray counts of this context's rows (R = row_end - row_begin
- * entries), collected while counters are on: the cost profile used to balance row strips
- * across GPUs. */
+/* Per-row work of this context's rows (R = row_end - row_begin entries), collected while
+ * row counters are on: segments + shadow rays (modes 3/4, simple AO kernel), or an estimate in
+ * sphere-test units (pooled AO kernel: per-sample setup + culled primary tests + bounce tests).
+ * The cost profile used to balance row strips across GPUs. */
 int rt_read_row_counters(rt_ctx* ctx, uint64_t* rows, int reset);
 
 /* ---- device math self-test (parity of the shared float semantics) ------------------ */

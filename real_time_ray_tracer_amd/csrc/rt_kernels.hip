@@ -351,6 +351,7 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4*
 // never accepted) and is skipped.
 // ---------------------------------------------------------------------------------------
 constexpr int kPool = 256;
+constexpr int kSetupCost = 24;  // per-sample setup (hashes, directions, shading) in sphere-test units
 
 // Float form of the same cull (no trig): cone axis a, cos/sin of the half-angle; a sphere
 // with inflated radius r_eff (r_eff^2 = r^2 + 1e-5 (d^2 + r^2)) lies outside the forward and
@@ -405,11 +406,11 @@ __device__ inline bool cone_misses_f(const ConeF& c, float4 g, float cx, float c
 // handed to idle lanes by ds_bpermute whenever lanes run out of work.  Bounce rounds then
 // run with (nearly) all lanes live, and no per-sample setup runs at partial utilisation.
 // ---------------------------------------------------------------------------------------
-template <int MINW, bool LAZY = true>
+template <int MINW, bool LAZY = true, int POOL = kPool>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   extern __shared__ float4 lds[];
   const int spp = P.spp, W = P.W, D = P.D, nobj = P.nobj;
-  const int TP = kPool / spp > 0 ? kPool / spp : 1;
+  const int TP = POOL / spp > 0 ? POOL / spp : 1;
   const int lane = threadIdx.x;
   float4* samp = lds;                      // [TP*spp] (r, g, b, stop value or -1)
   float4* prec = lds + TP * spp;           // [TP] first-segment (normal, t) of sample 0
@@ -459,7 +460,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       P.nrm[off] = z;
       P.dep[off] = z;  // (0, 0, 0, 0) / AA
       store_color(P, x, y, col);
-      if (P.row_counters) atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)spp);
+      if (P.row_counters) atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)spp);  // ~free
     }
     if (P.counters && lane == 0) {
       unsigned long long* c = P.counters + (blockIdx.x & (kCounterSlots - 1));
@@ -488,11 +489,13 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   const float inv_spp = 1.0f / (float)spp;
   // it / spp for pool items (< 2^16): exact via the float reciprocal (error << 0.5/spp)
   auto div_spp = [&](int it) { return (int)(((float)it + 0.5f) * inv_spp); };
+  // row cost profile (strip balancing), in sphere-test units: setup + culled primary + bounces
   auto finish = [&](int it, float r, float g, float b, float stopv, int segs) {
     samp[it] = make_float4(r, g, b, stopv);
     if (P.row_counters) {
       int y = P.trace_row0 + (int)((p0 + div_spp(it)) / W);
-      atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)segs);
+      atomicAdd(&P.row_counters[y - P.band_row0],
+                (unsigned long long)(kSetupCost + ncull + (segs - 1) * nobj));
     }
   };
 
@@ -815,18 +818,15 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
     // is the pooled, batch-prepared kernel (7) for all-sphere scenes.
     const char* ev = getenv("RTRT_AO_VARIANT");
     const int variant = ev ? atoi(ev) : 7;
-    if (all_spheres && variant == 7) {
+    if (all_spheres && (variant == 7 || variant == 11)) {
       const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
       const long long pools = (npix + TP - 1) / TP;
       const size_t psh = (size_t)TP * p.spp * sizeof(float4) + (size_t)TP * sizeof(float4) +
                          (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8;
-      hipLaunchKernelGGL(ao_batch_kernel<6>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
-    } else if (all_spheres && variant == 11) {  // same without the lazy shortcuts (A/B)
-      const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
-      const long long pools = (npix + TP - 1) / TP;
-      const size_t psh = (size_t)TP * p.spp * sizeof(float4) + (size_t)TP * sizeof(float4) +
-                         (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8;
-      hipLaunchKernelGGL((ao_batch_kernel<6, false>), dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+      if (variant == 11)  // without the lazy shortcuts (A/B)
+        hipLaunchKernelGGL((ao_batch_kernel<6, false>), dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+      else
+        hipLaunchKernelGGL(ao_batch_kernel<6>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
     } else if (!all_spheres)
       hipLaunchKernelGGL((ao_kernel<false, 0>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
     else if (variant == 2)

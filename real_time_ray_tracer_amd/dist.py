@@ -4,8 +4,9 @@ SURVEY.md §8e: every trace pixel is independent, so a frame is cut into N conti
 strips, one per GPU (one process per GPU, torch.distributed over RCCL/xGMI).  Each rank
 keeps its own g-buffer ring for its strip plus a 1-row halo (rendered redundantly, so the
 post-process needs no exchange); the only collective is the per-frame gather of the final
-image strips into rank 0.  Strip bounds are balanced by a per-row cost profile (segment
-counts from the kernels' row counters), because sky rows are far cheaper than ground rows.
+image strips into rank 0.  Strip bounds are balanced by a per-row cost profile (work
+estimates from the kernels' row counters), because sky rows are far cheaper than ground rows,
+then calibrated once against each strip's measured kernel time and re-balanced.
 
 The gather is pipelined: frame k's strip is gathered (async, RCCL stream) while frame k+1
 renders into the other of two image buffers.
@@ -39,6 +40,30 @@ def balanced_bounds(row_cost: np.ndarray, n: int, min_rows: int = 1) -> list[int
 
 def strip_cost(bounds: list[int], row_cost: np.ndarray) -> list[float]:
     return [float(np.sum(row_cost[bounds[i]:bounds[i + 1]])) for i in range(len(bounds) - 1)]
+
+
+def calibrate_row_cost(bounds: list[int], row_cost: np.ndarray, strip_time: list[float]) -> np.ndarray:
+    """Rescale the modelled per-row cost so every strip's total equals its measured time
+    (keeping the row shape inside each strip): corrects the cost model (setup vs test cost,
+    per-rank overheads) before a second balancing pass."""
+    c = np.asarray(row_cost, np.float64).copy()
+    for i in range(len(bounds) - 1):
+        a, b = bounds[i], bounds[i + 1]
+        tot = float(np.sum(c[a:b]))
+        t = float(strip_time[i])
+        if b <= a:
+            continue
+        if tot > 0:
+            c[a:b] *= t / tot
+        else:
+            c[a:b] = t / (b - a)
+    return c
+
+
+def imbalance(strip_time: list[float]) -> float:
+    """max / mean - 1 of the per-strip times."""
+    t = np.asarray(strip_time, np.float64)
+    return float(t.max() / max(t.mean(), 1e-30) - 1.0)
 
 
 @dataclass

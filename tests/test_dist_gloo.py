@@ -107,3 +107,31 @@ def test_balanced_bounds_equalise_cost():
     eq = strip_cost(equal_bounds(2160, 8), cost)
     assert max(eq) / np.mean(eq) > 1.5 > max(c) / np.mean(c)
     assert balanced_bounds(np.zeros(10), 3) == [0, 3, 7, 10] or len(balanced_bounds(np.zeros(10), 3)) == 4
+
+
+def test_calibration_corrects_a_wrong_cost_model():
+    """Modelled cost says sky rows cost 1, ground 9; the 'measured' truth is sky 0.1 and a
+    ground ramp 3..15, plus a fixed per-strip overhead on rank 0.  One calibration pass must bring the true
+    imbalance under a few percent."""
+    from real_time_ray_tracer_amd.dist import balanced_bounds, calibrate_row_cost, imbalance, strip_cost
+
+    H, n = 2160, 8
+    model = np.r_[np.full(1000, 1.0), np.full(1160, 9.0)]
+    truth = np.r_[np.full(1000, 0.1), np.linspace(3.0, 15.0, 1160)]
+
+    def measure(b):
+        t = strip_cost(b, truth)
+        t[0] += 300.0  # e.g. rank 0 also receives the gather
+        return t
+
+    b1 = balanced_bounds(model, n)
+    t1 = measure(b1)
+    assert imbalance(t1) > 0.1
+    b2 = balanced_bounds(calibrate_row_cost(b1, model, t1), n)
+    t2 = measure(b2)
+    assert imbalance(t2) < 0.03 and imbalance(t1) > 0.5
+    b3 = balanced_bounds(calibrate_row_cost(b2, calibrate_row_cost(b1, model, t1), t2), n)
+    assert imbalance(measure(b3)) < imbalance(t2)
+    # an empty-cost strip is spread uniformly, not divided by zero
+    c = calibrate_row_cost([0, 2, 4], np.zeros(4), [1.0, 3.0])
+    assert np.allclose(c, [0.5, 0.5, 1.5, 1.5])

@@ -16,8 +16,8 @@ cat "$OUT/bench.json"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
   python3 bench.py --config "$CFG" --steps 10 --warmup 8 --no-cpu-baseline > "$OUT/kt_bench.json" 2> "$OUT/kt.err"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-  python3 bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> "$OUT/pmc_fetch.err"
+  python3 bench.py --config "$CFG" --steps 3 --warmup 8 --no-cpu-baseline > /dev/null 2> "$OUT/pmc_fetch.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-  python3 bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> "$OUT/pmc_write.err"
+  python3 bench.py --config "$CFG" --steps 3 --warmup 8 --no-cpu-baseline > /dev/null 2> "$OUT/pmc_write.err"
 find "$OUT" -name "*.csv" | head -50
 python3 tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$CFG" "$OUT/pmc.json"
