@@ -148,10 +148,12 @@ int rt_read_row_counters(rt_ctx* ctx, uint64_t* rows, int reset);
 enum {
   RT_MATH_SIN = 0,       /* deterministic sin used by random() (in: x)                 */
   RT_MATH_RANDOM = 1,    /* random(vec2) hash, p_compute.glsl:65-75 (in: x,y pairs)    */
-  RT_MATH_SQRT = 2,      /* IEEE sqrtf (in: x)                                         */
+  RT_MATH_SQRT = 2,      /* IEEE sqrt as used by the kernels (in: x)                   */
   RT_MATH_DIV = 3,       /* IEEE a/b (in: a,b pairs)                                   */
   RT_MATH_NORMALIZE = 4, /* normalize(vec3) (in: xyz triples, out: xyz triples)        */
-  RT_MATH_SPHERE = 5     /* sphere_eval_ray (in: pos3,dir3,center3,r = 10 floats)      */
+  RT_MATH_SPHERE = 5,    /* sphere_eval_ray (in: pos3,dir3,center3,r = 10 floats)      */
+  RT_MATH_SQRT_SWEEP = 6 /* out[i] = #bit patterns in [i*in[0], (i+1)*in[0]) of the
+                            non-negative floats where the kernels' sqrt != sqrtf          */
 };
 int rt_selftest_math(rt_ctx* ctx, int fn, const float* in, float* out, size_t n);
 

@@ -60,6 +60,25 @@ __device__ __forceinline__ float det_sin(float x) {
   return (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
 }
 
+// IEEE binary32 square root, correctly rounded: the value sqrtf() has under
+// -fhip-fp32-correctly-rounded-divide-sqrt, written out so it stays a short straight-line
+// sequence: inputs below 2^-96 are scaled by 2^32, v_sqrt_f32 (<= 1 ulp) is corrected by one
+// ulp either way from the sign of the fma residuals, and the result is scaled back by 2^-16.
+// 0, +inf and NaN pass through.  Checked against sqrtf on every non-negative float
+// (tests/test_gpu_parity.py::test_sqrt_rn_exhaustive).
+__device__ __forceinline__ float sqrt_rn(float x) {
+  const bool tiny = x < 0x1p-96f;
+  const float xs = tiny ? x * 0x1p32f : x;
+  float s = __builtin_amdgcn_sqrtf(xs);
+  const float sm = __int_as_float(__float_as_int(s) - 1);
+  const float sp = __int_as_float(__float_as_int(s) + 1);
+  const float rm = fmaf(-sm, s, xs);
+  const float rp = fmaf(-sp, s, xs);
+  s = (rm <= 0.0f) ? sm : s;
+  s = (rp > 0.0f) ? sp : s;
+  return tiny ? s * 0x1p-16f : s;
+}
+
 // random(vec2), p_compute.glsl:65-75
 __device__ __forceinline__ float grandom(float sx, float sy) {
   float d = fmaf(sy, 78.233f, sx * 12.9898f);
@@ -154,19 +173,17 @@ __device__ __forceinline__ void sphere_candidate(f3 pos, f3 dir, float4 g, int i
   float b = dot(dir, pmc);
   float del = fmaf(g.w, g.w, fmaf(b, b, -dot(pmc, pmc)));
   if (del >= 0.0f) {
-    float res;
-    if (del == 0.0f) {
-      res = -1.0f * b;
-    } else {
-      float s = sqrtf(del);
-      float t1 = -1.0f * b + s;
-      float t2 = -1.0f * b - s;
-      res = (t2 < 0.0f) ? ((t1 < 0.0f) ? -1.0f : t1) : t2;
-    }
-    if (res > thr && (res < t || t < 0.0f)) {
-      t = res;
-      ind = i;
-    }
+    // One straight-line tail for del == 0 and del > 0: with s = sqrt(0) = 0 both roots are
+    // -b, so the reference's (del == 0 ? -b : root choice) differs only in values <= 0, and
+    // (t2 < 0 ? t1 : t2) differs from (t2 < 0 ? (t1 < 0 ? -1 : t1) : t2) only when t1 < 0:
+    // none of these is ever accepted (thr > 0).  Accepted t and index are unchanged.
+    float s = sqrt_rn(del);
+    float t1 = -1.0f * b + s;
+    float t2 = -1.0f * b - s;
+    float res = (t2 < 0.0f) ? t1 : t2;
+    const bool acc = (res > thr) & ((res < t) | (t < 0.0f));  // no short-circuit branches
+    t = acc ? res : t;
+    ind = acc ? i : ind;
   }
 }
 

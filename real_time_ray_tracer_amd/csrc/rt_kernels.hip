@@ -785,7 +785,19 @@ __global__ void selftest_kernel(int fn, const float* __restrict__ in, float* __r
   switch (fn) {
     case 0: out[i] = det_sin(in[i]); break;
     case 1: out[i] = grandom(in[2 * i], in[2 * i + 1]); break;
-    case 2: out[i] = sqrtf(in[i]); break;
+    case 2: out[i] = sqrt_rn(in[i]); break;
+    case 6: {  // exhaustive sqrt_rn == sqrtf over bit patterns [i*per, (i+1)*per) of [0, 0x7f800000]
+      const unsigned per = (unsigned)in[0];
+      unsigned bad = 0;
+      for (unsigned k = 0; k < per; ++k) {
+        unsigned long long u = (unsigned long long)i * per + k;
+        if (u > 0x7f800000ull) break;
+        float x = __uint_as_float((unsigned)u);
+        bad += __float_as_uint(sqrt_rn(x)) != __float_as_uint(sqrtf(x));
+      }
+      out[i] = (float)bad;
+      break;
+    }
     case 3: out[i] = in[2 * i] / in[2 * i + 1]; break;
     case 4: {
       f3 v = normalize(mk(in[3 * i], in[3 * i + 1], in[3 * i + 2]));

@@ -183,11 +183,23 @@ def test_math_primitives_bitwise():
     assert_bitwise(r.selftest_math(_lib.RT_MATH_SIN, x, x.size), ref, "det_sin")
     xy = rng.uniform(0, 8000, (20000, 2)).astype(np.float32)
     assert_bitwise(r.selftest_math(_lib.RT_MATH_RANDOM, xy, len(xy)), oracle.random2(xy), "random")
-    v = rng.uniform(0, 1e6, 100000).astype(np.float32)
+    v = np.concatenate([rng.uniform(0, 1e6, 100000), 10.0 ** rng.uniform(-45, 38.5, 100000),
+                        [0.0, -0.0, 1e-45, 1e-40, 2.0 ** -96, 2.0 ** -97, np.inf, 3.4e38]]).astype(np.float32)
     assert_bitwise(r.selftest_math(_lib.RT_MATH_SQRT, v, v.size), np.sqrt(v), "sqrt")
     ab = rng.uniform(-1e3, 1e3, (100000, 2)).astype(np.float32)
     assert_bitwise(r.selftest_math(_lib.RT_MATH_DIV, ab, len(ab)), ab[:, 0] / ab[:, 1], "div")
     r.close()
+
+
+def test_sqrt_rn_exhaustive():
+    """The kernels' explicit sqrt sequence equals sqrtf on every non-negative float
+    (0 .. +inf: 2^31 - 2^23 + 1 bit patterns), on the device."""
+    r = Renderer(8, 8, 1, 1)
+    per, n = 2048, 1 << 20
+    bad = r.selftest_math(_lib.RT_MATH_SQRT_SWEEP, np.array([per], np.float32), n)
+    r.close()
+    assert n * per > 0x7f800000
+    assert float(bad.sum()) == 0.0, f"{int(bad.sum())} mismatching inputs"
 
 
 def test_errors_are_reported():

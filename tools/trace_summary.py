@@ -1,0 +1,39 @@
+#!/usr/bin/env python
+"""Summarise a rocprofv3 kernel trace of `bench.py --warmup W --steps K` for profiles/:
+per-launch durations of the renderer's kernels in dispatch order and the mean over the timed
+launches (W warm-up first, then K timed, then the 2 counted frames), to compare with the
+bench line's live HIP-event kernel_ms.
+
+    python tools/trace_summary.py gpurun_out/<tag>/kt/run_kernel_trace.csv 8 10 "<command>"
+"""
+import csv
+import sys
+
+
+def main():
+    path, warm, steps = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    cmd = sys.argv[4] if len(sys.argv) > 4 else ""
+    launches = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            name = row["Kernel_Name"]
+            for key in ("ao_batch_kernel", "ao_kernel", "post_kernel", "phong_kernel", "hybrid_kernel"):
+                if key + "<" in name or key + "(" in name:
+                    d = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6
+                    launches.setdefault(key, []).append((int(row["Dispatch_Id"]), d, row["VGPR_Count"],
+                                                         row["SGPR_Count"], row["LDS_Block_Size"]))
+    if cmd:
+        print(cmd)
+    print(f"per-launch durations (ms), in dispatch order: {warm} warm-up, {steps} timed, 2 counted (work counters on)")
+    for key, ls in launches.items():
+        ls.sort()
+        ds = [d for _, d, *_ in ls]
+        timed = ds[warm:warm + steps]
+        print(f"{key}: vgpr={ls[0][2]} sgpr={ls[0][3]} lds={ls[0][4]}")
+        print(f"  all={[round(d, 3) for d in ds]}")
+        if timed:
+            print(f"  timed mean={sum(timed) / len(timed):.4f} ms")
+
+
+if __name__ == "__main__":
+    main()
