@@ -361,26 +361,33 @@ struct ConeF {
   float ax, ay, az, ct, st;
 };
 
+// The cone only has to be conservative, not bit-exact: it is built with the raw
+// v_rcp/v_sqrt/v_rsq instructions (<= 1 ulp, ~1e-7 relative), far inside the 2e-5 cosine
+// slack and the 1e-5 radius inflation.
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float fast_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
+
 __device__ inline ConeF pool_cone_f(const FrameParams& P, int xmin, int xmax, int ymin, int ymax) {
-  const float hps[2] = {((float)xmin - 0.1f) / P.W, ((float)xmax + 0.1f) / P.W};
-  const float vps[2] = {((float)ymin - 0.1f) / P.H, ((float)ymax + 0.1f) / P.H};
+  const float iw = fast_rcp((float)P.W), ih = fast_rcp((float)P.H);
+  const float hps[2] = {((float)xmin - 0.1f) * iw, ((float)xmax + 0.1f) * iw};
+  const float vps[2] = {((float)ymin - 0.1f) * ih, ((float)ymax + 0.1f) * ih};
   f3 d[4];
   f3 sum = mk(0.0f, 0.0f, 0.0f);
   for (int k = 0; k < 4; ++k) {
     float hp = hps[k & 1], vp = vps[k >> 1];
     f3 v = mk(P.lx + hp * P.hx + vp * P.vx, P.ly + hp * P.hy + vp * P.vy, P.lz + hp * P.hz + vp * P.vz);
-    float il = 1.0f / sqrtf(dot(v, v));
-    d[k] = il * v;
+    d[k] = fast_rsq(dot(v, v)) * v;
     sum = sum + d[k];
   }
-  float il = 1.0f / sqrtf(dot(sum, sum));
+  const float il = fast_rsq(dot(sum, sum));
   ConeF c;
   c.ax = sum.x * il; c.ay = sum.y * il; c.az = sum.z * il;
   float ct = 1.0f;
   for (int k = 0; k < 4; ++k) ct = fminf(ct, c.ax * d[k].x + c.ay * d[k].y + c.az * d[k].z);
   ct = fminf(fmaxf(ct - 2e-5f, -1.0f), 1.0f);  // widen the cone a little (direction rounding)
   c.ct = ct;
-  c.st = sqrtf(fmaxf(0.0f, 1.0f - ct * ct));
+  c.st = fast_sqrt(fmaxf(0.0f, 1.0f - ct * ct));
   return c;
 }
 
@@ -389,11 +396,12 @@ __device__ inline bool cone_misses_f(const ConeF& c, float4 g, float cx, float c
   float d2 = Lx * Lx + Ly * Ly + Lz * Lz, r2 = g.w * g.w;
   float reff2 = r2 + 1e-5f * (d2 + r2);
   if (!(d2 > reff2 * 1.01f + 1e-6f)) return false;  // camera inside / near the sphere: keep
-  float sa2 = reff2 / d2;
-  float sa = sqrtf(sa2), ca = sqrtf(1.0f - sa2);
+  float id = fast_rsq(d2);
+  float sa2 = reff2 * (id * id);
+  float sa = fast_sqrt(sa2), ca = fast_sqrt(fmaxf(0.0f, 1.0f - sa2));
   float K = c.ct * ca - c.st * sa - 2e-5f;  // cos(theta + alpha), made smaller (conservative)
   if (!(K > 0.0f)) return false;
-  float cphi = (c.ax * Lx + c.ay * Ly + c.az * Lz) / sqrtf(d2);
+  float cphi = (c.ax * Lx + c.ay * Ly + c.az * Lz) * id;
   return fabsf(cphi) < K;
 }
 
@@ -406,7 +414,7 @@ __device__ inline bool cone_misses_f(const ConeF& c, float4 g, float cx, float c
 // handed to idle lanes by ds_bpermute whenever lanes run out of work.  Bounce rounds then
 // run with (nearly) all lanes live, and no per-sample setup runs at partial utilisation.
 // ---------------------------------------------------------------------------------------
-template <int MINW, bool LAZY = true, int POOL = kPool>
+template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   extern __shared__ float4 lds[];
   const int spp = P.spp, W = P.W, D = P.D, nobj = P.nobj;
@@ -425,6 +433,16 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   const int np = (int)(npix - p0 < TP ? npix - p0 : TP);
   const int total = np * spp;
 
+  // ABL == 3: per-section wave clock (s_memtime) into the counters, timing ablation only
+  unsigned long long tsec[5] = {0, 0, 0, 0, 0};
+  unsigned long long tmark = ABL == 3 ? __builtin_amdgcn_s_memtime() : 0;
+  auto lap = [&](int k) {
+    if (ABL == 3) {
+      unsigned long long now = __builtin_amdgcn_s_memtime();
+      tsec[k] += now - tmark;
+      tmark = now;
+    }
+  };
   // ---- frustum cull of the primary rays -------------------------------------------------
   const int yf = P.trace_row0 + (int)(p0 / W), xf = (int)(p0 % W);
   const int yl = P.trace_row0 + (int)((p0 + np - 1) / W), xl = (int)((p0 + np - 1) % W);
@@ -441,6 +459,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     }
   }
   __syncthreads();
+  lap(0);
 
   if (LAZY && ncull == 0) {
     // Empty frustum: every primary ray of the pool provably misses every sphere, so each
@@ -586,6 +605,14 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           int i = (w << 6) + __builtin_ctzll(m);
           m &= m - 1;
           sphere_candidate(bpos, bdir, geo[i], i, 0.0001f, t, ind);
+          if (ABL == 2) {  // timing ablation: the culled primary tests twice
+            float z;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+            float t2 = -1.0f;
+            int i2 = -1;
+            sphere_candidate(mk(bpos.x + z, bpos.y, bpos.z), bdir, geo[i], i, 0.0001f, t2, i2);
+            if (i2 == 0x7fffffff) t = t2;
+          }
         }
       }
       ++nseg;
@@ -607,7 +634,9 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       if (need == 0) break;
       if (cursor >= nlive) {
         if (next >= total) break;
+        lap(2);
         prepare();
+        lap(1);
         continue;
       }
       int r = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
@@ -632,18 +661,27 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       cursor += take;
     }
     if (__ballot(has) == 0) break;
+    lap(2);
     // ---- one bounce segment for every live path, against every sphere ------------------
     exec_tests += (unsigned long long)nobj;
     if (has) {
       float t;
       int ind = closest_hit_pf(geo, nobj, pos, dir, 0.0001f, t);
+      if (ABL == 1) {  // timing ablation: the bounce tests twice
+        float z, t2;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        int i2 = closest_hit_pf(geo, nobj, mk(pos.x + z, pos.y, pos.z), dir, 0.0001f, t2);
+        if (i2 == 0x7fffffff) t = t2;
+      }
       ++nseg;
       has = shade(ind, t, pos, dir, hemi, rr, rg, rb, depth, item, false);
       depth -= 1;
     }
+    lap(3);
   }
+  lap(2);
 
-  if (P.counters) {
+  if (P.counters && ABL != 3) {
     unsigned sg = wave_sum(nseg);
     if (lane == 0) {
       unsigned long long* c = P.counters + (blockIdx.x & (kCounterSlots - 1));
@@ -684,6 +722,11 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
     P.dep[off] = d;
     store_color(P, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
+  }
+  if (ABL == 3 && P.counters && lane == 0) {
+    lap(4);
+    unsigned long long* c = P.counters + (blockIdx.x & (kCounterSlots - 1));
+    for (int k = 0; k < 5; ++k) atomicAdd(&c[k * kCounterSlots], tsec[k]);
   }
 }
 
@@ -830,13 +873,19 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
     // is the pooled, batch-prepared kernel (7) for all-sphere scenes.
     const char* ev = getenv("RTRT_AO_VARIANT");
     const int variant = ev ? atoi(ev) : 7;
-    if (all_spheres && (variant == 7 || variant == 11)) {
+    if (all_spheres && (variant == 7 || variant == 11 || (variant >= 91 && variant <= 93))) {
       const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
       const long long pools = (npix + TP - 1) / TP;
       const size_t psh = (size_t)TP * p.spp * sizeof(float4) + (size_t)TP * sizeof(float4) +
                          (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8;
       if (variant == 11)  // without the lazy shortcuts (A/B)
         hipLaunchKernelGGL((ao_batch_kernel<6, false>), dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+      else if (variant == 91)  // timing ablations: bounce tests / culled primary tests run twice
+        hipLaunchKernelGGL((ao_batch_kernel<6, true, kPool, 1>), dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+      else if (variant == 92)
+        hipLaunchKernelGGL((ao_batch_kernel<6, true, kPool, 2>), dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+      else if (variant == 93)  // per-section wave clocks into the counters (tools/sections.py)
+        hipLaunchKernelGGL((ao_batch_kernel<6, true, kPool, 3>), dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
       else
         hipLaunchKernelGGL(ao_batch_kernel<6>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
     } else if (!all_spheres)

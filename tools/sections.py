@@ -1,0 +1,49 @@
+#!/usr/bin/env python
+"""Where the pooled AO kernel's wave time goes: runs the ABL=3 build of ao_batch_kernel
+(RTRT_AO_VARIANT=93, s_memtime laps per section summed over waves) on a bench config.
+
+    python tools/sections.py --config d --frames 3
+"""
+import argparse
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+from bench import CONFIG_INDEX, CONFIGS  # noqa: E402
+from real_time_ray_tracer_amd import Header, Renderer, aspect_for  # noqa: E402
+
+NAMES = ["cull setup", "prepare (primary + first shade)", "hand-out / regeneration", "bounce test + shade",
+         "combine + stores"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="d")
+    ap.add_argument("--frames", type=int, default=3)
+    a = ap.parse_args()
+    W, H, S, spp, mode, _ = CONFIGS[a.config]
+    os.environ["RTRT_AO_VARIANT"] = "93"
+    h = Header.synthetic(S, spp, 1234 + CONFIG_INDEX[a.config], aspect_for(W, H))
+    r = Renderer(W, H, S, spp)
+    f = 0
+    for k in range(a.frames):
+        if k == a.frames - 1:
+            r.enable_counters(True)
+            r.read_counters(reset=True)
+        h.fill_rand_buffer(7000 + k)
+        h.set_mode(f, S)
+        r.upload_header(h)
+        f = r.dispatch(mode, f)
+    c = r.read_counters()
+    vals = [c["samples"], c["segments"], c["shadow_rays"], c["tests"], c["executed_lane_tests"]]
+    tot = sum(vals)
+    for n, v in zip(NAMES, vals):
+        print(f"{n:34s} {v / 1e9:9.3f} Gclk  {100 * v / tot:5.1f}%")
+    r.close()
+
+
+if __name__ == "__main__":
+    main()
