@@ -425,6 +425,9 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   int* pkind = (int*)(prec + TP);          // [TP]
   int* perm = pkind + ((TP + 1) & ~1);     // [64] live-rank -> lane of the prepared batch
   unsigned long long* cmask = (unsigned long long*)(perm + 64);  // [ceil(nobj/64)]
+  // [2*spp] rand_buffer staged in LDS (16-byte aligned after cmask)
+  float4* rls = (float4*)(((uintptr_t)(cmask + ((nobj + 63) >> 6)) + 15) & ~(uintptr_t)15);
+  for (int k = lane; k < 2 * spp; k += 64) rls[k] = P.rb[k];
   const float4* col = P.shapes + 2 * P.S;
   const float4* aux = P.shapes + 3 * P.S;
 
@@ -444,7 +447,18 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     }
   };
   // ---- frustum cull of the primary rays -------------------------------------------------
-  const int yf = P.trace_row0 + (int)(p0 / W), xf = (int)(p0 % W);
+  const int yf = P.trace_row0 + (int)(p0 / W), xf = (int)(p0 % W);  // once per pool (scalar)
+  // pixel lp of the pool: (xf + lp, yf), wrapped into the next row(s) when it passes W
+  auto pool_xy = [&](int lp, int& x, int& y) {
+    int xi = xf + lp;
+    y = yf;
+    if (xi >= W) {  // only pools that straddle a row end (none when TP divides W)
+      int q = (int)((unsigned)xi / (unsigned)W);
+      y += q;
+      xi -= q * W;
+    }
+    x = xi;
+  };
   const int yl = P.trace_row0 + (int)((p0 + np - 1) / W), xl = (int)((p0 + np - 1) % W);
   int ncull = 0;
   const int nwords = (nobj + 63) >> 6;
@@ -473,8 +487,8 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     const float4 col = gamma_out(sr / fa, sg / fa, sb / fa);
     const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     for (int lp = lane; lp < np; lp += 64) {
-      const long long pix = p0 + lp;
-      const int x = (int)(pix % W), y = P.trace_row0 + (int)(pix / W);
+      int x, y;
+      pool_xy(lp, x, y);
       const size_t off = (size_t)(y - P.band_row0) * W + x;
       P.nrm[off] = z;
       P.dep[off] = z;  // (0, 0, 0, 0) / AA
@@ -491,7 +505,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   }
 
   const f3 cam = mk(P.cx, P.cy, P.cz);
-  const float4* rbuf = P.rb;
+  const float4* rbuf = rls;
   // live path of this lane
   bool has = false;
   int item = 0, depth = 0;
@@ -512,7 +526,8 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   auto finish = [&](int it, float r, float g, float b, float stopv, int segs) {
     samp[it] = make_float4(r, g, b, stopv);
     if (P.row_counters) {
-      int y = P.trace_row0 + (int)((p0 + div_spp(it)) / W);
+      int x, y;
+      pool_xy(div_spp(it), x, y);
       atomicAdd(&P.row_counters[y - P.band_row0],
                 (unsigned long long)(kSetupCost + ncull + (segs - 1) * nobj));
     }
@@ -566,8 +581,8 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     exec_tests += (unsigned long long)ncull;
     if (bitem < total) {
       const int lp = div_spp(bitem), aa = bitem - lp * spp;
-      const long long pix = p0 + lp;
-      const int x = (int)(pix % W), y = P.trace_row0 + (int)(pix / W);
+      int x, y;
+      pool_xy(lp, x, y);
       const float px = (float)x, py = (float)y;
       float hp, vp;
       if (aa == 0) {
@@ -695,8 +710,8 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
 
   // ---- sample combine in aa order (ao_compute.glsl:303-339) ----------------------------
   for (int lp = lane; lp < np; lp += 64) {
-    const long long pix = p0 + lp;
-    const int x = (int)(pix % W), y = P.trace_row0 + (int)(pix / W);
+    int x, y;
+    pool_xy(lp, x, y);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f, ystop = -1.0f;
     const float4* ps = samp + lp * spp;
     for (int k = 0; k < spp; ++k) {
@@ -877,7 +892,8 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
       const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
       const long long pools = (npix + TP - 1) / TP;
       const size_t psh = (size_t)TP * p.spp * sizeof(float4) + (size_t)TP * sizeof(float4) +
-                         (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8;
+                         (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8 +
+                         16 + (size_t)2 * p.spp * sizeof(float4);
       if (variant == 11)  // without the lazy shortcuts (A/B)
         hipLaunchKernelGGL((ao_batch_kernel<6, false>), dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
       else if (variant == 91)  // timing ablations: bounce tests / culled primary tests run twice
