@@ -69,7 +69,7 @@ typedef struct {
   int num_shapes; /* NUM_SHAPES (src/main.cpp:34): capacity of simple_shapes[S][5]      */
   int spp;        /* AA (src/main.cpp:31): samples per pixel; rand_buffer has 2*spp vec4 */
   int num_frames; /* NUM_FRAMES (src/main.cpp:36): g-buffer ring length, normally 8     */
-  int max_depth;  /* RECURSION_DEPTH (resources/ao_compute.glsl:10): path length cap, 20 */
+  int max_depth;  /* RECURSION_DEPTH (resources/ao_compute.glsl:10): path length cap, 20 (<= 65535) */
   int row_begin;  /* this context renders frame rows [row_begin, row_end);              */
   int row_end;    /*   row_begin = row_end = 0 means the whole frame                    */
 } rt_config;

@@ -420,14 +420,17 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   const int spp = P.spp, W = P.W, D = P.D, nobj = P.nobj;
   const int TP = POOL / spp > 0 ? POOL / spp : 1;
   const int lane = threadIdx.x;
-  float4* samp = lds;                      // [TP*spp] (r, g, b, stop value or -1)
-  float4* prec = lds + TP * spp;           // [TP] first-segment (normal, t) of sample 0
-  int* pkind = (int*)(prec + TP);          // [TP]
+  const int NS = TP * spp;
+  float4* prec = lds;                      // [TP] first-segment (normal, t) of sample 0
+  float* sres = (float*)(prec + TP);       // [3][NS] per-sample r, g, b (channel-major)
+  int* pstop = (int*)(sres + 3 * NS);      // [TP] max (aa << 16 | stop value) of the samples with a stop write
+  int* pkind = pstop + TP;                 // [TP]
   int* perm = pkind + ((TP + 1) & ~1);     // [64] live-rank -> lane of the prepared batch
   unsigned long long* cmask = (unsigned long long*)(perm + 64);  // [ceil(nobj/64)]
   // [2*spp] rand_buffer staged in LDS (16-byte aligned after cmask)
   float4* rls = (float4*)(((uintptr_t)(cmask + ((nobj + 63) >> 6)) + 15) & ~(uintptr_t)15);
   for (int k = lane; k < 2 * spp; k += 64) rls[k] = P.rb[k];
+  for (int k = lane; k < TP; k += 64) pstop[k] = -1;
   const float4* col = P.shapes + 2 * P.S;
   const float4* aux = P.shapes + 3 * P.S;
 
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   const int total = np * spp;
 
   // ABL == 3: per-section wave clock (s_memtime) into the counters, timing ablation only
-  unsigned long long tsec[5] = {0, 0, 0, 0, 0};
+  unsigned long long tsec[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // 5..7: bounce rounds, sum ncull, prepares
   unsigned long long tmark = ABL == 3 ? __builtin_amdgcn_s_memtime() : 0;
   auto lap = [&](int k) {
     if (ABL == 3) {
@@ -524,7 +527,13 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   auto div_spp = [&](int it) { return (int)(((float)it + 0.5f) * inv_spp); };
   // row cost profile (strip balancing), in sphere-test units: setup + culled primary + bounces
   auto finish = [&](int it, float r, float g, float b, float stopv, int segs) {
-    samp[it] = make_float4(r, g, b, stopv);
+    sres[it] = r;
+    sres[NS + it] = g;
+    sres[2 * NS + it] = b;
+    if (stopv >= 0.0f) {  // depth_buffer.y: the last writer in sample order wins
+      const int lq = div_spp(it);
+      atomicMax(&pstop[lq], ((it - lq * spp) << 16) | (int)stopv);
+    }
     if (P.row_counters) {
       int x, y;
       pool_xy(div_spp(it), x, y);
@@ -578,6 +587,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   auto prepare = [&]() {
     bitem = next + lane;
     bool live = false;
+    if (ABL == 3) { tsec[6] += (unsigned long long)ncull; tsec[7] += 1; }
     exec_tests += (unsigned long long)ncull;
     if (bitem < total) {
       const int lp = div_spp(bitem), aa = bitem - lp * spp;
@@ -677,6 +687,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     }
     if (__ballot(has) == 0) break;
     lap(2);
+    if (ABL == 3) tsec[5] += 1;
     // ---- one bounce segment for every live path, against every sphere ------------------
     exec_tests += (unsigned long long)nobj;
     if (has) {
@@ -712,13 +723,13 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   for (int lp = lane; lp < np; lp += 64) {
     int x, y;
     pool_xy(lp, x, y);
-    float sr = 0.0f, sg = 0.0f, sb = 0.0f, ystop = -1.0f;
-    const float4* ps = samp + lp * spp;
+    float sr = 0.0f, sg = 0.0f, sb = 0.0f;
+    const float* ps = sres + lp * spp;
     for (int k = 0; k < spp; ++k) {
-      float4 q = ps[k];
-      sr = sr + q.x; sg = sg + q.y; sb = sb + q.z;
-      if (q.w >= 0.0f) ystop = q.w;
+      sr = sr + ps[k]; sg = sg + ps[NS + k]; sb = sb + ps[2 * NS + k];
     }
+    const int st = pstop[lp];
+    const float ystop = st < 0 ? -1.0f : (float)(st & 0xffff);
     const float fa = (float)spp;
     const size_t off = (size_t)(y - P.band_row0) * W + x;
     const int kind = pkind[lp];
@@ -741,7 +752,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   if (ABL == 3 && P.counters && lane == 0) {
     lap(4);
     unsigned long long* c = P.counters + (blockIdx.x & (kCounterSlots - 1));
-    for (int k = 0; k < 5; ++k) atomicAdd(&c[k * kCounterSlots], tsec[k]);
+    for (int k = 0; k < 8; ++k) atomicAdd(&c[k * kCounterSlots], tsec[k]);
   }
 }
 
@@ -888,22 +899,26 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
     // is the pooled, batch-prepared kernel (7) for all-sphere scenes.
     const char* ev = getenv("RTRT_AO_VARIANT");
     const int variant = ev ? atoi(ev) : 7;
-    if (all_spheres && (variant == 7 || variant == 11 || (variant >= 91 && variant <= 93))) {
-      const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
+    if (all_spheres && (variant == 7 || variant == 11 || variant == 12 || (variant >= 91 && variant <= 93))) {
+      const int pool = variant == 12 ? 384 : kPool;
+      const int TP = pool / p.spp > 0 ? pool / p.spp : 1;
       const long long pools = (npix + TP - 1) / TP;
-      const size_t psh = (size_t)TP * p.spp * sizeof(float4) + (size_t)TP * sizeof(float4) +
+      const size_t psh = (size_t)TP * sizeof(float4) + (size_t)3 * TP * p.spp * sizeof(float) + (size_t)TP * sizeof(int) +
                          (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8 +
                          16 + (size_t)2 * p.spp * sizeof(float4);
+      const dim3 g((unsigned)pools), b(64);
       if (variant == 11)  // without the lazy shortcuts (A/B)
-        hipLaunchKernelGGL((ao_batch_kernel<6, false>), dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+        hipLaunchKernelGGL((ao_batch_kernel<6, false>), g, b, psh, stream, p, p.shapes);
+      else if (variant == 12)  // pool of 384 samples (A/B)
+        hipLaunchKernelGGL((ao_batch_kernel<6, true, 384>), g, b, psh, stream, p, p.shapes);
       else if (variant == 91)  // timing ablations: bounce tests / culled primary tests run twice
-        hipLaunchKernelGGL((ao_batch_kernel<6, true, kPool, 1>), dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+        hipLaunchKernelGGL((ao_batch_kernel<6, true, kPool, 1>), g, b, psh, stream, p, p.shapes);
       else if (variant == 92)
-        hipLaunchKernelGGL((ao_batch_kernel<6, true, kPool, 2>), dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+        hipLaunchKernelGGL((ao_batch_kernel<6, true, kPool, 2>), g, b, psh, stream, p, p.shapes);
       else if (variant == 93)  // per-section wave clocks into the counters (tools/sections.py)
-        hipLaunchKernelGGL((ao_batch_kernel<6, true, kPool, 3>), dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+        hipLaunchKernelGGL((ao_batch_kernel<6, true, kPool, 3>), g, b, psh, stream, p, p.shapes);
       else
-        hipLaunchKernelGGL(ao_batch_kernel<6>, dim3((unsigned)pools), dim3(64), psh, stream, p, p.shapes);
+        hipLaunchKernelGGL(ao_batch_kernel<6>, g, b, psh, stream, p, p.shapes);
     } else if (!all_spheres)
       hipLaunchKernelGGL((ao_kernel<false, 0>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
     else if (variant == 2)

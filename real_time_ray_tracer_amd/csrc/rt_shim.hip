@@ -26,6 +26,7 @@ namespace {
 
 constexpr int kMaxShapes = 2048;
 constexpr int kMaxSpp = 256;
+constexpr int kMaxDepth = 65535;  // stop values are packed in 16 bits by the pooled AO kernel
 constexpr int kStageSlots = 8;
 
 struct Stage {
@@ -294,7 +295,7 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
   if (c.max_depth == 0) c.max_depth = RT_RECURSION_DEPTH;
   if (c.row_begin == 0 && c.row_end == 0) c.row_end = c.height;
   if (c.width <= 0 || c.height <= 0 || c.num_shapes < 0 || c.num_shapes > kMaxShapes || c.spp <= 0 ||
-      c.spp > kMaxSpp || c.num_frames <= 0 || c.num_frames > rt::kMaxFrames || c.max_depth <= 0 ||
+      c.spp > kMaxSpp || c.num_frames <= 0 || c.num_frames > rt::kMaxFrames || c.max_depth <= 0 || c.max_depth > kMaxDepth ||
       c.row_begin < 0 || c.row_end > c.height || c.row_begin >= c.row_end)
     return RT_E_INVAL;
   int ndev = 0;

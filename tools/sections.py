@@ -36,13 +36,34 @@ def main():
         h.fill_rand_buffer(7000 + k)
         h.set_mode(f, S)
         r.upload_header(h)
-        f = r.dispatch(mode, f)
+        f = r.dispatch(2 if mode == 1 else mode, f)  # AO pass only: counters 5..7 are the kernel's
     c = r.read_counters()
     vals = [c["samples"], c["segments"], c["shadow_rays"], c["tests"], c["executed_lane_tests"]]
     tot = sum(vals)
     for n, v in zip(NAMES, vals):
         print(f"{n:34s} {v / 1e9:9.3f} Gclk  {100 * v / tot:5.1f}%")
+    rounds, sum_ncull, prepares = c["post_pixels"], c["history_read"], c["history_accepted"]
+    print(f"bounce rounds {rounds}  prepares {prepares}  mean culled primary set {sum_ncull / max(prepares, 1):.2f}")
+    print(f"bounce sphere-iterations per frame {rounds * S / 1e6:.1f} M; per 64-sample prepare batch "
+          f"{rounds / max(prepares, 1):.2f} rounds")
     r.close()
+    # the default kernel's work counters on the same frames: useful bounce segments
+    os.environ["RTRT_AO_VARIANT"] = "7"
+    r = Renderer(W, H, S, spp)
+    f = 0
+    for k in range(a.frames):
+        if k == a.frames - 1:
+            r.enable_counters(True)
+            r.read_counters(reset=True)
+        h.fill_rand_buffer(7000 + k)
+        h.set_mode(f, S)
+        r.upload_header(h)
+        f = r.dispatch(2 if mode == 1 else mode, f)
+    c2 = r.read_counters()
+    r.close()
+    bounce = c2["segments"] - c2["samples"]
+    print(f"useful bounce segments {bounce / 1e6:.1f} M = {bounce / max(rounds * 64, 1):.3f} of bounce lane slots; "
+          f"samples {c2['samples'] / 1e6:.1f} M; executed lane-tests {c2['executed_lane_tests'] / 1e9:.2f} G")
 
 
 if __name__ == "__main__":
