@@ -899,7 +899,7 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
     // is the pooled, batch-prepared kernel (7) for all-sphere scenes.
     const char* ev = getenv("RTRT_AO_VARIANT");
     const int variant = ev ? atoi(ev) : 7;
-    if (all_spheres && (variant == 7 || variant == 11 || variant == 12 || (variant >= 91 && variant <= 93))) {
+    if (all_spheres && (variant == 7 || variant == 11 || variant == 12 || variant == 13 || variant == 14 || (variant >= 91 && variant <= 93))) {
       const int pool = variant == 12 ? 384 : kPool;
       const int TP = pool / p.spp > 0 ? pool / p.spp : 1;
       const long long pools = (npix + TP - 1) / TP;
@@ -908,17 +908,21 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
                          16 + (size_t)2 * p.spp * sizeof(float4);
       const dim3 g((unsigned)pools), b(64);
       if (variant == 11)  // without the lazy shortcuts (A/B)
-        hipLaunchKernelGGL((ao_batch_kernel<6, false>), g, b, psh, stream, p, p.shapes);
+        hipLaunchKernelGGL((ao_batch_kernel<7, false>), g, b, psh, stream, p, p.shapes);
       else if (variant == 12)  // pool of 384 samples (A/B)
-        hipLaunchKernelGGL((ao_batch_kernel<6, true, 384>), g, b, psh, stream, p, p.shapes);
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, 384>), g, b, psh, stream, p, p.shapes);
+      else if (variant == 13)  // 8 waves/SIMD register budget (A/B)
+        hipLaunchKernelGGL((ao_batch_kernel<8, true>), g, b, psh, stream, p, p.shapes);
+      else if (variant == 14)  // 6 waves/SIMD register budget (A/B)
+        hipLaunchKernelGGL((ao_batch_kernel<6, true>), g, b, psh, stream, p, p.shapes);
       else if (variant == 91)  // timing ablations: bounce tests / culled primary tests run twice
-        hipLaunchKernelGGL((ao_batch_kernel<6, true, kPool, 1>), g, b, psh, stream, p, p.shapes);
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 1>), g, b, psh, stream, p, p.shapes);
       else if (variant == 92)
-        hipLaunchKernelGGL((ao_batch_kernel<6, true, kPool, 2>), g, b, psh, stream, p, p.shapes);
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2>), g, b, psh, stream, p, p.shapes);
       else if (variant == 93)  // per-section wave clocks into the counters (tools/sections.py)
-        hipLaunchKernelGGL((ao_batch_kernel<6, true, kPool, 3>), g, b, psh, stream, p, p.shapes);
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3>), g, b, psh, stream, p, p.shapes);
       else
-        hipLaunchKernelGGL(ao_batch_kernel<6>, g, b, psh, stream, p, p.shapes);
+        hipLaunchKernelGGL(ao_batch_kernel<7>, g, b, psh, stream, p, p.shapes);
     } else if (!all_spheres)
       hipLaunchKernelGGL((ao_kernel<false, 0>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
     else if (variant == 2)
