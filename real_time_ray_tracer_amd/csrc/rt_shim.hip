@@ -155,6 +155,9 @@ void fill_params(const rt_ctx* c, int frame, rt::FrameParams& p) {
   p.nobj = c->nobj;
   p.S = c->cfg.num_shapes;
   p.spp = c->cfg.spp;
+  p.inv_spp = 1.0f / (float)c->cfg.spp;
+  p.fW = (float)c->cfg.width;
+  p.fH = (float)c->cfg.height;
   p.D = c->cfg.max_depth;
   p.F = c->cfg.num_frames;
   p.frame = frame;

@@ -71,15 +71,17 @@ def test_full_size_band_parity(cfg, frames, rows):
     r.close()
 
 
-@pytest.mark.parametrize("variant", ["0", "2"])
+@pytest.mark.parametrize("variant", ["0", "2", "20", "21", "22"])
 def test_fallback_ao_kernels_match_oracle(variant, monkeypatch):
-    """The simple lane-per-sample AO kernels (used for scenes with planes, or forced) agree too."""
+    """The other AO kernels agree too: the simple lane-per-sample ones (used for scenes with
+    planes, or forced: 0, 2) and the streaming sub-pool ones (20-22)."""
     from test_gpu_parity import make_header, run_both
 
     monkeypatch.setenv("RTRT_AO_VARIANT", variant)
     W, H = 48, 32
-    for scene in ("syn16", "s6"):
-        h = make_header(scene, W, H, 4)
+    for scene, spp in (("syn16", 4), ("s6", 4), ("syn16", 16), ("syn12", 3), ("empty", 4)):
+        h = make_header(scene, W, H, spp)
         g, s, img = run_both(h, W, H, 1, 3)
         assert_close(g.image, img, f"variant {variant} {scene}")
         assert_bitwise(g.depth, s.depth, f"variant {variant} {scene} depth")
+        assert_bitwise(g.normals, s.normals, f"variant {variant} {scene} normals")
