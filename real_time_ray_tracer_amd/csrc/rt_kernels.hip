@@ -769,14 +769,14 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
 // (in sample order, as ao_compute.glsl:303-339) as soon as all its samples are done.  Same
 // per-sample arithmetic, culling, shading and combine as ao_batch_kernel (bit-identical).
 // ---------------------------------------------------------------------------------------
-__host__ __device__ constexpr size_t stream_lds_bytes(int spp, int nobj, int SUB, int R) {
+__host__ __device__ constexpr size_t stream_lds_bytes(int spp, int nobj, int SUB, int R, int K) {
   return (size_t)R * (SUB / spp > 0 ? SUB / spp : 1) * (16 + 4 + 4) +            // prec, pstop, pkind
          (size_t)3 * R * (SUB / spp > 0 ? SUB / spp : 1) * spp * 4 +              // sres
-         (size_t)2 * R * 4 + 64 * 4 + 8 + (size_t)R * ((nobj + 63) / 64) * 8 +   // sdone, sncull, perm, cmask
-         16 + (size_t)2 * spp * 16;                                               // rls
+         (size_t)R * 4 + (size_t)K * 4 + 64 * 4 + 8 +                             // sdone, sncull, perm
+         (size_t)K * ((nobj + 63) / 64) * 8 + 16 + (size_t)2 * spp * 16;          // cmask, rls
 }
 
-template <int MINW, int SUB, int R>
+template <int MINW, int SUB, int R, int CG = 2>
 __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, const float4* __restrict__ geo, int K,
                                                              float inv_tps) {
   extern __shared__ float4 lds[];
@@ -790,10 +790,10 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
   int* pstop = (int*)(sres + 3 * R * SUBN);        // [R*TPs] max (aa << 16 | stop value)
   int* pkind = pstop + R * TPs;                    // [R*TPs]
   int* sdone = pkind + R * TPs;                    // [R] finished samples of the slot's sub-pool
-  int* sncull = sdone + R;                         // [R] culled-set size (-1: empty frustum)
-  int* perm = sncull + R;                          // [64] live-rank -> lane of the prepared batch
-  unsigned long long* cmask = (unsigned long long*)(((uintptr_t)(perm + 64) + 7) & ~(uintptr_t)7);  // [R][nwords]
-  float4* rls = (float4*)(((uintptr_t)(cmask + R * nwords) + 15) & ~(uintptr_t)15);                // [2*spp]
+  int* sncull = sdone + R;                         // [K] culled-set size per sub-pool (-1: empty frustum)
+  int* perm = sncull + K;                          // [64] live-rank -> lane of the prepared batch
+  unsigned long long* cmask = (unsigned long long*)(((uintptr_t)(perm + 64) + 7) & ~(uintptr_t)7);  // [K][nwords]
+  float4* rls = (float4*)(((uintptr_t)(cmask + K * nwords) + 15) & ~(uintptr_t)15);                // [2*spp]
   for (int k = lane; k < 2 * spp; k += 64) rls[k] = P.rb[k];
   for (int k = lane; k < R * TPs; k += 64) pstop[k] = -1;
   if (lane < R) sdone[lane] = 0;
@@ -837,9 +837,10 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
   unsigned long long exec_tests = 0, fast_samples = 0;
 
   // ---- sub-pool j: frustum cull (and the empty-frustum fast path) -------------------------
-  auto cull = [&](int j) -> bool {
-    const int s = j % R;
-    const int a = j * TPs, e = (j + 1) * TPs < npw ? (j + 1) * TPs : npw;
+  // cone cull of sub-pools [j0, j1) together (one cone over their pixels; a superset of each
+  // sub-pool's own cone, so still conservative), and the empty-frustum fast path
+  auto cull = [&](int j0, int j1) {
+    const int a = j0 * TPs, e = j1 * TPs < npw ? j1 * TPs : npw;
     int xa, ya, xe, ye;
     pool_xy(a, xa, ya);
     pool_xy(e - 1, xe, ye);
@@ -850,13 +851,12 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
       bool keep = i < nobj && !cone_misses_f(cone, geo[i], P.cx, P.cy, P.cz);
       unsigned long long m = __ballot(keep);
       nc += __popcll(m);
-      if (lane == 0) cmask[s * nwords + w] = m;
+      if (lane == 0)
+        for (int j = j0; j < j1; ++j) cmask[j * nwords + w] = m;
     }
     const bool fast = nc == 0;
-    if (lane == 0) {
-      sncull[s] = fast ? -1 : nc;
-      if (fast) sdone[s] = sub_count(j);
-    }
+    if (lane == 0)
+      for (int j = j0; j < j1; ++j) sncull[j] = fast ? -1 : nc;
     if (fast) {  // every primary ray misses every sphere: as ao_batch_kernel's fast path
       const float fa = (float)spp;
       float sr = 0.0f, sg = 0.0f, sb = 0.0f;
@@ -874,16 +874,21 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
         store_color(P, x, y, c);
         if (P.row_counters) atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)spp);
       }
-      fast_samples += (unsigned long long)sub_count(j);
+      for (int j = j0; j < j1; ++j) fast_samples += (unsigned long long)sub_count(j);
     }
-    __syncthreads();
-    return fast;
   };
+  // every sub-pool's cull up front (and the empty ones written), before any path is live
+  {
+    const int nsub = (npw + TPs - 1) / TPs;
+    const int cg = CG > 0 ? CG : 1;  // sub-pools per cone
+    for (int j = 0; j < nsub; j += cg) cull(j, j + cg < nsub ? j + cg : nsub);
+    __syncthreads();
+  }
 
   // ---- sub-pool j: combine in sample order and free its slot -----------------------------
   auto combine = [&](int j) {
     const int s = j % R;
-    if (__builtin_amdgcn_readfirstlane(sncull[s]) >= 0) {
+    if (__builtin_amdgcn_readfirstlane(sncull[j]) >= 0) {
       const int a = j * TPs, e = (j + 1) * TPs < npw ? (j + 1) * TPs : npw;
       const float* base = sres + s * SUBN;
       for (int lq = lane; lq < e - a; lq += 64) {
@@ -928,11 +933,10 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
     sres[R * SUBN + k] = g;
     sres[2 * R * SUBN + k] = b;
     if (stopv >= 0.0f) atomicMax(&pstop[s * TPs + (lp - j * TPs)], ((it - lp * spp) << 16) | (int)stopv);
-    atomicAdd(&sdone[s], 1);
     if (P.row_counters) {
       int x, y;
       pool_xy(lp, x, y);
-      atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)(kSetupCost + sncull[s] + (segs - 1) * nobj));
+      atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)(kSetupCost + sncull[j] + (segs - 1) * nobj));
     }
   };
 
@@ -982,7 +986,7 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
     const int s = j % R;
     const int jend = (j + 1) * SUBN < totalw ? (j + 1) * SUBN : totalw;
     const int bend = next + 64 < jend ? next + 64 : jend;
-    const int ncull = __builtin_amdgcn_readfirstlane(sncull[s]);
+    const int ncull = __builtin_amdgcn_readfirstlane(sncull[j]);
     bitem = next + lane;
     bool live = false;
     exec_tests += (unsigned long long)ncull;
@@ -1009,7 +1013,7 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
       float t = -1.0f;
       int ind = -1;
       for (int w = 0; w < nwords; ++w) {
-        unsigned long long m = cmask[s * nwords + w];
+        unsigned long long m = cmask[j * nwords + w];
         m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
             (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
         while (m) {
@@ -1028,6 +1032,8 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
       }
       live = shade(ind, t, bpos, bdir, bhemi, br, bg, bb, D, bitem, true);
     }
+    const unsigned long long fm = __ballot(bitem < bend && !live);  // ended at the primary hit
+    if (lane == 0 && fm) sdone[s] += __popcll(fm);
     unsigned long long lm = __ballot(live);
     if (live) perm[__builtin_amdgcn_mbcnt_hi((unsigned)(lm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)lm, 0u))] = lane;
     nlive = __popcll(lm);
@@ -1051,7 +1057,8 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
         if (j >= jcomb + R) break;  // ring full: run the stragglers' bounce rounds first
         if (j > jcull) {
           jcull = j;
-          if (cull(j)) {
+          if (__builtin_amdgcn_readfirstlane(sncull[j]) < 0) {  // empty frustum: written up front
+            if (lane == 0) sdone[j % R] = sub_count(j);
             next = (j + 1) * SUBN < totalw ? (j + 1) * SUBN : totalw;
             continue;
           }
@@ -1084,12 +1091,19 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
       continue;  // the ring was full and every path has ended: the retire step frees it
     }
     exec_tests += (unsigned long long)nobj;
+    const bool had = has;
+    const int myslot = div_tps(div_spp(item)) % R;
     if (has) {
       float t;
       int ind = closest_hit_pf(geo, nobj, pos, dir, 0.0001f, t);
       ++nseg;
       has = shade(ind, t, pos, dir, hemi, rr, rg, rb, depth, item, false);
       depth -= 1;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {  // finished samples per ring slot, one LDS add per slot
+      const unsigned long long fm = __ballot(had && !has && myslot == r);
+      if (lane == 0 && fm) sdone[r] += __popcll(fm);
     }
   }
   while (jcomb <= jcull) {  // drain: every remaining sub-pool is complete
@@ -1253,8 +1267,8 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
     // is the pooled, batch-prepared kernel (7) for all-sphere scenes.
     const char* ev = getenv("RTRT_AO_VARIANT");
     const int variant = ev ? atoi(ev) : 7;
-    if (all_spheres && (variant == 7 || variant == 11 || variant == 12 || variant == 13 || variant == 14 || (variant >= 91 && variant <= 93))) {
-      const int pool = variant == 12 ? 384 : kPool;
+    if (all_spheres && (variant == 7 || variant == 11 || variant == 12 || variant == 13 || variant == 14 || variant == 15 || (variant >= 91 && variant <= 93))) {
+      const int pool = variant == 12 ? 384 : (variant == 15 ? 512 : kPool);
       const int TP = pool / p.spp > 0 ? pool / p.spp : 1;
       const long long pools = (npix + TP - 1) / TP;
       const size_t psh = (size_t)TP * sizeof(float4) + (size_t)3 * TP * p.spp * sizeof(float) + (size_t)TP * sizeof(int) +
@@ -1265,6 +1279,8 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
         hipLaunchKernelGGL((ao_batch_kernel<7, false>), g, b, psh, stream, p, p.shapes);
       else if (variant == 12)  // pool of 384 samples (A/B)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, 384>), g, b, psh, stream, p, p.shapes);
+      else if (variant == 15)  // pool of 512 samples (A/B)
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, 512>), g, b, psh, stream, p, p.shapes);
       else if (variant == 13)  // 8 waves/SIMD register budget (A/B)
         hipLaunchKernelGGL((ao_batch_kernel<8, true>), g, b, psh, stream, p, p.shapes);
       else if (variant == 14)  // 6 waves/SIMD register budget (A/B)
@@ -1277,21 +1293,23 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3>), g, b, psh, stream, p, p.shapes);
       else
         hipLaunchKernelGGL(ao_batch_kernel<7>, g, b, psh, stream, p, p.shapes);
-    } else if (all_spheres && variant >= 20 && variant <= 25) {
+    } else if (all_spheres && variant >= 20 && variant <= 26) {
       // streaming sub-pools (A/B): 20: SUB 128 R 2, 21: 128/3, 22: 64/4, 23: 128/2 K 16, 24: 128/2 K 4
       const int K = variant == 23 ? 16 : (variant == 24 ? 4 : 8);
       const int sub = variant == 22 ? 64 : 128;
       const int TPs = sub / p.spp > 0 ? sub / p.spp : 1;
       const long long waves = (npix + (long long)K * TPs - 1) / ((long long)K * TPs);
       const dim3 g((unsigned)waves), b(64);
-      if (variant == 25)
-        hipLaunchKernelGGL((ao_stream_kernel<6, 128, 2>), g, b, stream_lds_bytes(p.spp, p.nobj, 128, 2), stream, p, p.shapes, K, 1.0f / (float)TPs);
+      if (variant == 26)
+        hipLaunchKernelGGL((ao_stream_kernel<6, 128, 2, 1>), g, b, stream_lds_bytes(p.spp, p.nobj, 128, 2, K), stream, p, p.shapes, K, 1.0f / (float)TPs);
+      else if (variant == 25)
+        hipLaunchKernelGGL((ao_stream_kernel<6, 128, 2>), g, b, stream_lds_bytes(p.spp, p.nobj, 128, 2, K), stream, p, p.shapes, K, 1.0f / (float)TPs);
       else if (variant == 21)
-        hipLaunchKernelGGL((ao_stream_kernel<7, 128, 3>), g, b, stream_lds_bytes(p.spp, p.nobj, 128, 3), stream, p, p.shapes, K, 1.0f / (float)TPs);
+        hipLaunchKernelGGL((ao_stream_kernel<7, 128, 3>), g, b, stream_lds_bytes(p.spp, p.nobj, 128, 3, K), stream, p, p.shapes, K, 1.0f / (float)TPs);
       else if (variant == 22)
-        hipLaunchKernelGGL((ao_stream_kernel<7, 64, 4>), g, b, stream_lds_bytes(p.spp, p.nobj, 64, 4), stream, p, p.shapes, K, 1.0f / (float)TPs);
+        hipLaunchKernelGGL((ao_stream_kernel<7, 64, 4>), g, b, stream_lds_bytes(p.spp, p.nobj, 64, 4, K), stream, p, p.shapes, K, 1.0f / (float)TPs);
       else
-        hipLaunchKernelGGL((ao_stream_kernel<7, 128, 2>), g, b, stream_lds_bytes(p.spp, p.nobj, 128, 2), stream, p, p.shapes, K, 1.0f / (float)TPs);
+        hipLaunchKernelGGL((ao_stream_kernel<7, 128, 2>), g, b, stream_lds_bytes(p.spp, p.nobj, 128, 2, K), stream, p, p.shapes, K, 1.0f / (float)TPs);
     } else if (!all_spheres)
       hipLaunchKernelGGL((ao_kernel<false, 0>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
     else if (variant == 2)
