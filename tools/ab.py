@@ -28,11 +28,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--frames", type=int, default=4)
     ap.add_argument("--env", default="RTRT_AO_VARIANT")
+    ap.add_argument("--prog", type=int, default=0, help="program to time (default: the trace pass)")
+    ap.add_argument("--time-from", type=int, default=1, help="first frame timed (history fills over 8 frames)")
     args = ap.parse_args()
     W, H, S, spp, mode, desc = CONFIGS[args.config]
     variants = [v for v in args.variants.split(",")]
     h = Header.synthetic(S, spp, 1234 + CONFIG_INDEX[args.config], aspect_for(W, H))
-    prog = {1: 1, 2: 3, 3: 4, 4: 5}[mode]
+    prog = args.prog or {1: 1, 2: 3, 3: 4, 4: 5}[mode]
     times = {v: [] for v in variants}
     ref_img = None
     counts = None
@@ -47,7 +49,7 @@ def main():
                 h.fill_rand_buffer(7000 + k)
                 h.set_mode(f, S)
                 r.upload_header(h)
-                if k == 1:
+                if k == args.time_from:
                     r.enable_timing(True)
                 f = r.dispatch(mode, f)
             n, ms = r.kernel_stats(prog)
