@@ -1263,53 +1263,40 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
     const long long npix = (long long)p.trace_rows * p.W;
     const long long grid = (npix + ppb - 1) / ppb;
     const size_t sh = lds + (size_t)block * sizeof(float4);
-    // RTRT_AO_VARIANT: internal A/B switch for kernel experiments (tools/ab.py); the default
-    // is the pooled, batch-prepared kernel (7) for all-sphere scenes.
+    // RTRT_AO_VARIANT: internal A/B switch for kernel experiments (tools/ab.py).
+    // Default 7: the pooled, batch-prepared kernel for all-sphere scenes.  11: without the
+    // lazy shortcuts.  20/25: the streaming sub-pool kernel (7 / 6 waves).  91-93: timing
+    // ablations (bounce tests twice, culled primary tests twice, section clocks).  0/2: the
+    // lane-per-sample kernel (the general one, used for scenes with planes).
     const char* ev = getenv("RTRT_AO_VARIANT");
     const int variant = ev ? atoi(ev) : 7;
-    if (all_spheres && (variant == 7 || variant == 11 || variant == 12 || variant == 13 || variant == 14 || variant == 15 || (variant >= 91 && variant <= 93))) {
-      const int pool = variant == 12 ? 384 : (variant == 15 ? 512 : kPool);
-      const int TP = pool / p.spp > 0 ? pool / p.spp : 1;
+    if (all_spheres && (variant == 7 || variant == 11 || (variant >= 91 && variant <= 93))) {
+      const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
       const long long pools = (npix + TP - 1) / TP;
       const size_t psh = (size_t)TP * sizeof(float4) + (size_t)3 * TP * p.spp * sizeof(float) + (size_t)TP * sizeof(int) +
                          (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8 +
                          16 + (size_t)2 * p.spp * sizeof(float4);
       const dim3 g((unsigned)pools), b(64);
-      if (variant == 11)  // without the lazy shortcuts (A/B)
+      if (variant == 11)
         hipLaunchKernelGGL((ao_batch_kernel<7, false>), g, b, psh, stream, p, p.shapes);
-      else if (variant == 12)  // pool of 384 samples (A/B)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, 384>), g, b, psh, stream, p, p.shapes);
-      else if (variant == 15)  // pool of 512 samples (A/B)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, 512>), g, b, psh, stream, p, p.shapes);
-      else if (variant == 13)  // 8 waves/SIMD register budget (A/B)
-        hipLaunchKernelGGL((ao_batch_kernel<8, true>), g, b, psh, stream, p, p.shapes);
-      else if (variant == 14)  // 6 waves/SIMD register budget (A/B)
-        hipLaunchKernelGGL((ao_batch_kernel<6, true>), g, b, psh, stream, p, p.shapes);
-      else if (variant == 91)  // timing ablations: bounce tests / culled primary tests run twice
+      else if (variant == 91)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 1>), g, b, psh, stream, p, p.shapes);
       else if (variant == 92)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2>), g, b, psh, stream, p, p.shapes);
-      else if (variant == 93)  // per-section wave clocks into the counters (tools/sections.py)
+      else if (variant == 93)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3>), g, b, psh, stream, p, p.shapes);
       else
         hipLaunchKernelGGL(ao_batch_kernel<7>, g, b, psh, stream, p, p.shapes);
-    } else if (all_spheres && variant >= 20 && variant <= 26) {
-      // streaming sub-pools (A/B): 20: SUB 128 R 2, 21: 128/3, 22: 64/4, 23: 128/2 K 16, 24: 128/2 K 4
-      const int K = variant == 23 ? 16 : (variant == 24 ? 4 : 8);
-      const int sub = variant == 22 ? 64 : 128;
-      const int TPs = sub / p.spp > 0 ? sub / p.spp : 1;
-      const long long waves = (npix + (long long)K * TPs - 1) / ((long long)K * TPs);
+    } else if (all_spheres && (variant == 20 || variant == 25)) {
+      constexpr int kSub = 128, kRing = 2, kWaveSub = 8;  // sub-pool samples, ring slots, sub-pools per wave
+      const int TPs = kSub / p.spp > 0 ? kSub / p.spp : 1;
+      const long long waves = (npix + (long long)kWaveSub * TPs - 1) / ((long long)kWaveSub * TPs);
       const dim3 g((unsigned)waves), b(64);
-      if (variant == 26)
-        hipLaunchKernelGGL((ao_stream_kernel<6, 128, 2, 1>), g, b, stream_lds_bytes(p.spp, p.nobj, 128, 2, K), stream, p, p.shapes, K, 1.0f / (float)TPs);
-      else if (variant == 25)
-        hipLaunchKernelGGL((ao_stream_kernel<6, 128, 2>), g, b, stream_lds_bytes(p.spp, p.nobj, 128, 2, K), stream, p, p.shapes, K, 1.0f / (float)TPs);
-      else if (variant == 21)
-        hipLaunchKernelGGL((ao_stream_kernel<7, 128, 3>), g, b, stream_lds_bytes(p.spp, p.nobj, 128, 3, K), stream, p, p.shapes, K, 1.0f / (float)TPs);
-      else if (variant == 22)
-        hipLaunchKernelGGL((ao_stream_kernel<7, 64, 4>), g, b, stream_lds_bytes(p.spp, p.nobj, 64, 4, K), stream, p, p.shapes, K, 1.0f / (float)TPs);
+      const size_t sh2 = stream_lds_bytes(p.spp, p.nobj, kSub, kRing, kWaveSub);
+      if (variant == 25)
+        hipLaunchKernelGGL((ao_stream_kernel<6, kSub, kRing>), g, b, sh2, stream, p, p.shapes, kWaveSub, 1.0f / (float)TPs);
       else
-        hipLaunchKernelGGL((ao_stream_kernel<7, 128, 2>), g, b, stream_lds_bytes(p.spp, p.nobj, 128, 2, K), stream, p, p.shapes, K, 1.0f / (float)TPs);
+        hipLaunchKernelGGL((ao_stream_kernel<7, kSub, kRing>), g, b, sh2, stream, p, p.shapes, kWaveSub, 1.0f / (float)TPs);
     } else if (!all_spheres)
       hipLaunchKernelGGL((ao_kernel<false, 0>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
     else if (variant == 2)

@@ -71,10 +71,11 @@ def test_full_size_band_parity(cfg, frames, rows):
     r.close()
 
 
-@pytest.mark.parametrize("variant", ["0", "2", "20", "21", "22"])
+@pytest.mark.parametrize("variant", ["0", "2", "11", "20", "25"])
 def test_fallback_ao_kernels_match_oracle(variant, monkeypatch):
     """The other AO kernels agree too: the simple lane-per-sample ones (used for scenes with
-    planes, or forced: 0, 2) and the streaming sub-pool ones (20-22)."""
+    planes, or forced: 0, 2), the pooled kernel without lazy shortcuts (11) and the streaming
+    sub-pool kernels (20, 25)."""
     from test_gpu_parity import make_header, run_both
 
     monkeypatch.setenv("RTRT_AO_VARIANT", variant)
