@@ -144,7 +144,7 @@ def main():
     torch.cuda.set_stream(stream)
 
     # ---- strip plan: cost-balanced from the kernels' per-row work counters, then calibrated
-    # against each strip's measured kernel time (two passes) ------------------------------------
+    # against each strip's measured kernel time (best of three measured plans) ------------------
     bounds = equal_bounds(H, world)
     balance_info = None
     if world > 1 and not args.no_balance:
@@ -158,7 +158,7 @@ def main():
                 header.fill_rand_buffer(7000 + k) if mode in (1, 2) else header.moving_light(False)
                 header.set_mode(f, S)
                 r.upload_header(header)
-                if k == frames - 2 and not counters:
+                if k == frames - 3 and not counters:  # time the last 3 frames
                     r.enable_timing(True)
                     r.reset_stats()
                 f = r.dispatch(mode, f)
@@ -177,20 +177,24 @@ def main():
         dist.all_reduce(full)
         row_cost = full.cpu().numpy()
         bounds = balanced_bounds(row_cost, world)
-        # calibration: time each strip (kernels only), rescale the profile, re-balance; twice
-        t_model = None
-        for _ in range(2):
-            _, ms = strip_run(bounds, 4 if mode in (1, 2) else 2, False)
+        # calibration: time each strip's kernels, rescale the profile so every strip's total is
+        # its measured time, re-balance; keep the best of the measured plans (3 measurements)
+        measured = []
+        for it in range(3):
+            _, ms = strip_run(bounds, 6 if mode in (1, 2) else 3, False)
             tt = torch.zeros(world, dtype=torch.float64, device=cdev)
             tt[rank] = ms
             dist.all_reduce(tt)
             t1 = tt.cpu().tolist()
-            if t_model is None:
-                t_model = (list(bounds), t1)
-            row_cost = calibrate_row_cost(bounds, row_cost, t1)
-            bounds = balanced_bounds(row_cost, world)
-        balance_info = {"model_bounds": t_model[0], "model_strip_ms": [round(t, 4) for t in t_model[1]],
-                        "model_imbalance": round(imbalance(t_model[1]), 4)}
+            measured.append((max(t1), list(bounds), t1))
+            if it < 2:
+                row_cost = calibrate_row_cost(bounds, row_cost, t1)
+                bounds = balanced_bounds(row_cost, world)
+        best = min(measured, key=lambda m: m[0])
+        bounds = best[1]
+        balance_info = {"model_bounds": measured[0][1], "model_strip_ms": [round(t, 4) for t in measured[0][2]],
+                        "model_imbalance": round(imbalance(measured[0][2]), 4),
+                        "calibrated_max_ms": [round(m[0], 4) for m in measured]}
     plan = StripPlan(W, H, bounds)
     r0, r1 = plan.rows(rank)
     rend = Renderer(W, H, S, spp, device=gpu, rows=(r0, r1))
