@@ -43,6 +43,8 @@ SIGNATURES = {
     "rt_set_stream": (C.c_int, [_ctx, _vp]),
     "rt_use_own_stream": (C.c_int, [_ctx]),
     "rt_get_stream": (_vp, [_ctx]),
+    "rt_enable_pipelining": (C.c_int, [_ctx, C.c_int, _vp]),
+    "rt_get_output_stream": (_vp, [_ctx]),
     "rt_synchronize": (C.c_int, [_ctx]),
     "rt_last_hip_error": (C.c_int, [_ctx]),
     "rt_upload_header": (C.c_int, [_ctx, _vp, C.c_size_t]),

@@ -30,6 +30,8 @@ struct FrameParams {
   float4* out_pix;           // colour destination [band_rows][W]
   float4* nrm;               // normals_buffer slot `frame` [band_rows][W]
   float4* dep;               // depth_buffer slot `frame`
+  const float4* nrm_prev;    // the slot's previous normals / depth (stale reads); == nrm / dep
+  const float4* dep_prev;    // unless the frame is pipelined (written to a fresh buffer)
   float4* image;             // [img_rows][W] or nullptr
   const float4* raw;         // post-process input (pre-filter snapshot of slot `frame`)
   const float4* hist_pix[kMaxFrames];  // per slot

@@ -339,7 +339,10 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4*
     d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     P.nrm[off] = d;
   } else {
-    d = P.dep[off];  // stale: sample 0 hit an emissive shape first (no g-buffer write)
+    // stale: sample 0 hit an emissive shape first (no g-buffer write): the slot keeps its
+    // previous normal and depth (read from the slot's previous buffers when pipelined)
+    d = P.dep_prev[off];
+    if (P.nrm_prev != P.nrm) P.nrm[off] = P.nrm_prev[off];
   }
   if (ystop >= 0.0f) d.y = ystop;
   d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
@@ -745,8 +748,9 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     } else if (kind == PRIM_MISS) {
       d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       P.nrm[off] = d;
-    } else {
-      d = P.dep[off];
+    } else {  // stale (see ao_kernel)
+      d = P.dep_prev[off];
+      if (P.nrm_prev != P.nrm) P.nrm[off] = P.nrm_prev[off];
     }
     if (ystop >= 0.0f) d.y = ystop;
     d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
@@ -912,8 +916,9 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
         } else if (kind == PRIM_MISS) {
           d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
           P.nrm[off] = d;
-        } else {
-          d = P.dep[off];
+        } else {  // stale (see ao_kernel)
+          d = P.dep_prev[off];
+          if (P.nrm_prev != P.nrm) P.nrm[off] = P.nrm_prev[off];
         }
         if (ystop >= 0.0f) d.y = ystop;
         d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;

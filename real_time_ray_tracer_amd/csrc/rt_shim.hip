@@ -6,9 +6,17 @@
 //   compute_two_shaders (622-671)             -> rt_compute_two_shaders
 //   compute() (553-578)                       -> rt_dispatch
 // Device layout: the g-buffer ring stays resident in HBM as per-slot row-major [rows][W]
-// float4 arrays (pixels has one spare slot buffer so the post-process can write out of
-// place and swap), instead of the reference's 2 x 55.76 MB host round trip per frame.  The
-// reference [F][W][H] layout is produced only by rt_download / consumed by rt_upload_gbuffer.
+// float4 arrays, each reached through a slot -> buffer map with spare buffers (pixels: two,
+// so the post-process can write out of place and swap; normals/depth: one), instead of the
+// reference's 2 x 55.76 MB host round trip per frame.  The reference [F][W][H] layout is
+// produced only by rt_download / consumed by rt_upload_gbuffer.
+//
+// Pipelined mode 1 (rt_enable_pipelining): frame k's post-process runs on a second stream
+// while frame k+1's AO pass runs.  AO k+1 writes its normals/depth into the spare buffers and
+// its raw pixels into one of the two spare pixel buffers, so the post-process of frame k,
+// which may read slot (k+1)%8's previous contents as its oldest history, never sees them
+// change; AO k waits for post k-2 (the last reader of the buffers it overwrites).  The
+// results are those of the sequential order, bit for bit.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -47,10 +55,19 @@ struct rt_ctx {
   hipStream_t stream = nullptr;
   float4* d_shapes = nullptr;  // [4][S]
   float4* d_rb = nullptr;      // [2*spp]
-  std::vector<float4*> pix;    // F+1 buffers
+  std::vector<float4*> pix;    // F+2 buffers
   std::vector<int> pix_slot;   // slot -> buffer index
-  int spare = 0;
-  std::vector<float4*> nrm, dep;
+  int spare = 0, spare2 = 0;   // pixel buffers outside the map
+  std::vector<float4*> nrm, dep;       // F+1 buffers each
+  std::vector<int> nrm_slot, dep_slot;  // slot -> buffer index
+  int nrm_spare = 0, dep_spare = 0;
+  // pipelined mode 1
+  bool pipelined = false;
+  hipStream_t out_stream = nullptr, own_out_stream = nullptr;
+  hipEvent_t ev_ao = nullptr, ev_post[2] = {nullptr, nullptr}, ev_join = nullptr;
+  bool post_recorded[2] = {false, false};
+  long long pipe_n = 0;
+  bool out_pending = false;
   float4* d_image_own = nullptr;
   float4* d_image = nullptr;
   std::vector<float> header;   // host copy of the SSBO prefix
@@ -62,7 +79,7 @@ struct rt_ctx {
   int stage_next = 0;
   // timing
   bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[RT_PROG_COUNT];
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[RT_PROG_COUNT];  // recorded on the launch stream
   std::vector<hipEvent_t> event_pool;
   double total_ms[RT_PROG_COUNT] = {};
   int launches[RT_PROG_COUNT] = {};
@@ -139,7 +156,28 @@ void free_all(rt_ctx* c) {
   if (c->d_rb) (void)hipFree(c->d_rb);
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->d_row_counters) (void)hipFree(c->d_row_counters);
+  for (auto e : {c->ev_ao, c->ev_post[0], c->ev_post[1], c->ev_join})
+    if (e) (void)hipEventDestroy(e);
+  if (c->own_out_stream) (void)hipStreamDestroy(c->own_out_stream);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+}
+
+// Order everything issued so far on the output stream before later work on the main stream
+// (every call except a pipelined mode-1 dispatch starts with this).
+int join(rt_ctx* c) {
+  if (!c->out_pending) return RT_OK;
+  RT_HIP(c, hipEventRecord(c->ev_join, c->out_stream));
+  RT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+  c->out_pending = false;
+  c->post_recorded[0] = c->post_recorded[1] = false;  // ordered by the join from now on
+  c->pipe_n = 0;
+  return RT_OK;
+}
+
+int sync_all(rt_ctx* c) {
+  RT_HIP(c, hipStreamSynchronize(c->stream));
+  if (c->out_stream && c->out_stream != c->stream) RT_HIP(c, hipStreamSynchronize(c->out_stream));
+  return RT_OK;
 }
 
 const float* hv(const rt_ctx* c, int v) { return c->header.data() + 4 * v; }
@@ -175,36 +213,41 @@ void fill_params(const rt_ctx* c, int frame, rt::FrameParams& p) {
   p.image = c->d_image;
   for (int s = 0; s < c->cfg.num_frames; ++s) {
     p.hist_pix[s] = c->pix[c->pix_slot[s]];
-    p.hist_nrm[s] = c->nrm[s];
-    p.hist_dep[s] = c->dep[s];
+    p.hist_nrm[s] = c->nrm[c->nrm_slot[s]];
+    p.hist_dep[s] = c->dep[c->dep_slot[s]];
   }
-  p.nrm = c->nrm[frame];
-  p.dep = c->dep[frame];
+  p.nrm = c->nrm[c->nrm_slot[frame]];
+  p.dep = c->dep[c->dep_slot[frame]];
+  p.nrm_prev = p.nrm;
+  p.dep_prev = p.dep;
   p.counters = c->counting ? c->d_counters : nullptr;
   p.row_counters = c->row_counting ? c->d_row_counters : nullptr;
 }
 
-int launch(rt_ctx* c, int program, const rt::FrameParams& p) {
+int launch(rt_ctx* c, int program, const rt::FrameParams& p, hipStream_t st) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->timing) {
     e0 = get_event(c);
     e1 = get_event(c);
     if (!e0 || !e1) return RT_E_HIP;
-    RT_HIP(c, hipEventRecord(e0, c->stream));
+    RT_HIP(c, hipEventRecord(e0, st));
   }
-  hipError_t e = rt::launch_program(program, p, c->all_spheres, c->stream);
+  hipError_t e = rt::launch_program(program, p, c->all_spheres, st);
   if (e != hipSuccess) return hip_fail(c, e);
   if (c->timing) {
-    RT_HIP(c, hipEventRecord(e1, c->stream));
+    RT_HIP(c, hipEventRecord(e1, st));
     c->pending[program].emplace_back(e0, e1);
   }
   return RT_OK;
 }
+int launch(rt_ctx* c, int program, const rt::FrameParams& p) { return launch(c, program, p, c->stream); }
 
 int run_program(rt_ctx* c, int program, int frame) {
   if (!c->have_header) return RT_E_STATE;
   if (frame < 0 || frame >= c->cfg.num_frames) return RT_E_INVAL;
   RT_HIP(c, hipSetDevice(c->device));
+  int jr = join(c);
+  if (jr != RT_OK) return jr;
   rt::FrameParams p;
   fill_params(c, frame, p);
   switch (program) {
@@ -239,11 +282,52 @@ int run_program(rt_ctx* c, int program, int frame) {
   }
 }
 
+// One pipelined mode-1 frame (see the header comment): AO on the main stream into fresh
+// normals/depth and a raw pixel buffer, post-process on the output stream.
+int pipelined_frame(rt_ctx* c, int frame) {
+  if (!c->have_header) return RT_E_STATE;
+  if (frame < 0 || frame >= c->cfg.num_frames) return RT_E_INVAL;
+  RT_HIP(c, hipSetDevice(c->device));
+  const int n2 = (int)(c->pipe_n & 1);
+  if (c->post_recorded[n2]) RT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_post[n2], 0));  // post k-2
+  float4* raw = c->pix[n2 ? c->spare2 : c->spare];
+  rt::FrameParams p;
+  fill_params(c, frame, p);
+  p.trace_row0 = c->band0;
+  p.trace_rows = c->band_rows;
+  p.out_pix = raw;
+  p.image = nullptr;
+  p.nrm_prev = p.nrm;  // the slot's previous contents (stale reads)
+  p.dep_prev = p.dep;
+  p.nrm = c->nrm[c->nrm_spare];
+  p.dep = c->dep[c->dep_spare];
+  int rc = launch(c, RT_PROG_AOP_COMPUTE, p, c->stream);
+  if (rc != RT_OK) return rc;
+  std::swap(c->nrm_slot[frame], c->nrm_spare);
+  std::swap(c->dep_slot[frame], c->dep_spare);
+  RT_HIP(c, hipEventRecord(c->ev_ao, c->stream));
+  RT_HIP(c, hipStreamWaitEvent(c->out_stream, c->ev_ao, 0));
+  rt::FrameParams q;
+  fill_params(c, frame, q);
+  q.trace_row0 = c->own0;
+  q.trace_rows = c->own_rows;
+  q.raw = raw;
+  q.out_pix = c->pix[c->pix_slot[frame]];  // filtered in place of slot `frame`'s oldest contents
+  rc = launch(c, RT_PROG_AOP_POSTPROCESSING, q, c->out_stream);
+  if (rc != RT_OK) return rc;
+  RT_HIP(c, hipEventRecord(c->ev_post[n2], c->out_stream));
+  c->post_recorded[n2] = true;
+  c->out_pending = true;
+  c->pipe_n += 1;
+  return RT_OK;
+}
+
 int resolve_timing(rt_ctx* c) {
   bool any = false;
   for (int k = 0; k < RT_PROG_COUNT; ++k) any = any || !c->pending[k].empty();
   if (!any) return RT_OK;
-  RT_HIP(c, hipStreamSynchronize(c->stream));
+  int rc = sync_all(c);
+  if (rc != RT_OK) return rc;
   for (int k = 0; k < RT_PROG_COUNT; ++k) {
     for (auto& pr : c->pending[k]) {
       float ms = 0.0f;
@@ -323,16 +407,18 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
   const size_t slot = slot_elems(x) * sizeof(float4);
   const int F = c.num_frames;
   if (e == hipSuccess) {
-    x->pix.assign(F + 1, nullptr);
-    x->nrm.assign(F, nullptr);
-    x->dep.assign(F, nullptr);
-    for (int k = 0; k <= F && e == hipSuccess; ++k) e = hipMalloc(&x->pix[k], slot);
-    for (int k = 0; k < F && e == hipSuccess; ++k) e = hipMalloc(&x->nrm[k], slot);
-    for (int k = 0; k < F && e == hipSuccess; ++k) e = hipMalloc(&x->dep[k], slot);
+    x->pix.assign(F + 2, nullptr);
+    x->nrm.assign(F + 1, nullptr);
+    x->dep.assign(F + 1, nullptr);
+    for (int k = 0; k < F + 2 && e == hipSuccess; ++k) e = hipMalloc(&x->pix[k], slot);
+    for (int k = 0; k < F + 1 && e == hipSuccess; ++k) e = hipMalloc(&x->nrm[k], slot);
+    for (int k = 0; k < F + 1 && e == hipSuccess; ++k) e = hipMalloc(&x->dep[k], slot);
     // value-initialised ssbo_CPUMEM: the ring starts at zero
-    for (int k = 0; k <= F && e == hipSuccess; ++k) e = hipMemsetAsync(x->pix[k], 0, slot, x->stream);
-    for (int k = 0; k < F && e == hipSuccess; ++k) e = hipMemsetAsync(x->nrm[k], 0, slot, x->stream);
-    for (int k = 0; k < F && e == hipSuccess; ++k) e = hipMemsetAsync(x->dep[k], 0, slot, x->stream);
+    for (int k = 0; k < F + 2 && e == hipSuccess; ++k) e = hipMemsetAsync(x->pix[k], 0, slot, x->stream);
+    for (int k = 0; k < F + 1 && e == hipSuccess; ++k) e = hipMemsetAsync(x->nrm[k], 0, slot, x->stream);
+    for (int k = 0; k < F + 1 && e == hipSuccess; ++k) e = hipMemsetAsync(x->dep[k], 0, slot, x->stream);
+    for (hipEvent_t* ev : {&x->ev_ao, &x->ev_post[0], &x->ev_post[1], &x->ev_join})
+      if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipMalloc(&x->d_image_own, (size_t)x->own_rows * c.width * sizeof(float4));
   if (e == hipSuccess) e = hipMemsetAsync(x->d_image_own, 0, (size_t)x->own_rows * c.width * sizeof(float4), x->stream);
@@ -347,8 +433,13 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
   }
   x->d_image = x->d_image_own;
   x->pix_slot.resize(F);
-  for (int k = 0; k < F; ++k) x->pix_slot[k] = k;
+  x->nrm_slot.resize(F);
+  x->dep_slot.resize(F);
+  for (int k = 0; k < F; ++k) x->pix_slot[k] = x->nrm_slot[k] = x->dep_slot[k] = k;
   x->spare = F;
+  x->spare2 = F + 1;
+  x->nrm_spare = x->dep_spare = F;
+  x->out_stream = x->own_stream;
   x->header.assign(rt_header_bytes(c.num_shapes, c.spp) / 4, 0.0f);
   x->table.assign((size_t)4 * std::max(1, c.num_shapes), make_float4(0, 0, 0, 0));
   *out = x;
@@ -358,7 +449,7 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
 int rt_destroy(rt_ctx* c) {
   if (!c) return RT_E_INVAL;
   (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)sync_all(c);
   free_all(c);
   delete c;
   return RT_OK;
@@ -367,25 +458,52 @@ int rt_destroy(rt_ctx* c) {
 int rt_set_stream(rt_ctx* c, void* s) {
   if (!c) return RT_E_INVAL;
   RT_HIP(c, hipSetDevice(c->device));
-  RT_HIP(c, hipStreamSynchronize(c->stream));
+  int rc = sync_all(c);
+  if (rc != RT_OK) return rc;
+  c->out_pending = false;
+  c->post_recorded[0] = c->post_recorded[1] = false;
+  c->pipe_n = 0;
   c->stream = (hipStream_t)s;  // NULL = the legacy NULL stream
+  if (!c->pipelined) c->out_stream = c->stream;
   return RT_OK;
 }
 
 int rt_use_own_stream(rt_ctx* c) {
   if (!c) return RT_E_INVAL;
+  return rt_set_stream(c, (void*)c->own_stream);
+}
+
+int rt_enable_pipelining(rt_ctx* c, int on, void* output_stream) {
+  if (!c) return RT_E_INVAL;
   RT_HIP(c, hipSetDevice(c->device));
-  RT_HIP(c, hipStreamSynchronize(c->stream));
-  c->stream = c->own_stream;
+  int rc = sync_all(c);
+  if (rc != RT_OK) return rc;
+  c->out_pending = false;
+  c->post_recorded[0] = c->post_recorded[1] = false;
+  c->pipe_n = 0;
+  c->pipelined = on != 0;
+  if (!c->pipelined) {
+    c->out_stream = c->stream;
+    return RT_OK;
+  }
+  if (output_stream) {
+    c->out_stream = (hipStream_t)output_stream;
+  } else {
+    if (!c->own_out_stream) RT_HIP(c, hipStreamCreateWithFlags(&c->own_out_stream, hipStreamNonBlocking));
+    c->out_stream = c->own_out_stream;
+  }
+  if (c->out_stream == c->stream) c->pipelined = false;  // one stream: nothing to overlap
   return RT_OK;
 }
+
+void* rt_get_output_stream(rt_ctx* c) { return c ? (void*)c->out_stream : nullptr; }
 
 void* rt_get_stream(rt_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int rt_synchronize(rt_ctx* c) {
   if (!c) return RT_E_INVAL;
-  RT_HIP(c, hipStreamSynchronize(c->stream));
-  return RT_OK;
+  RT_HIP(c, hipSetDevice(c->device));
+  return sync_all(c);
 }
 
 int rt_last_hip_error(rt_ctx* c) { return c ? c->last_hip : 0; }
@@ -441,6 +559,10 @@ int rt_dispatch(rt_ctx* c, int mode, int frame) {
   int rc;
   switch (mode) {
     case RT_MODE_AO_PP:
+      if (c->pipelined) {
+        rc = pipelined_frame(c, frame);
+        break;
+      }
       rc = run_program(c, RT_PROG_AOP_COMPUTE, frame);
       if (rc == RT_OK) rc = run_program(c, RT_PROG_AOP_POSTPROCESSING, frame);
       break;
@@ -460,18 +582,20 @@ int rt_download(rt_ctx* c, float* pixels, float* normals, float* depth, float* i
   const size_t slot = slot_elems(c);
   const size_t ref_slot = (size_t)c->cfg.width * c->own_rows * 4;
   std::vector<float> tmp(slot * 4);
-  RT_HIP(c, hipStreamSynchronize(c->stream));
+  int rc = join(c);
+  if (rc == RT_OK) rc = sync_all(c);
+  if (rc != RT_OK) return rc;
   for (int f = 0; f < F; ++f) {
     if (pixels) {
       RT_HIP(c, hipMemcpy(tmp.data(), c->pix[c->pix_slot[f]], slot * 16, hipMemcpyDeviceToHost));
       dev_to_ref(c, tmp.data(), pixels + f * ref_slot);
     }
     if (normals) {
-      RT_HIP(c, hipMemcpy(tmp.data(), c->nrm[f], slot * 16, hipMemcpyDeviceToHost));
+      RT_HIP(c, hipMemcpy(tmp.data(), c->nrm[c->nrm_slot[f]], slot * 16, hipMemcpyDeviceToHost));
       dev_to_ref(c, tmp.data(), normals + f * ref_slot);
     }
     if (depth) {
-      RT_HIP(c, hipMemcpy(tmp.data(), c->dep[f], slot * 16, hipMemcpyDeviceToHost));
+      RT_HIP(c, hipMemcpy(tmp.data(), c->dep[c->dep_slot[f]], slot * 16, hipMemcpyDeviceToHost));
       dev_to_ref(c, tmp.data(), depth + f * ref_slot);
     }
   }
@@ -487,10 +611,12 @@ int rt_upload_gbuffer(rt_ctx* c, const float* pixels, const float* normals, cons
   const size_t slot = slot_elems(c);
   const size_t ref_slot = (size_t)c->cfg.width * c->own_rows * 4;
   std::vector<float> tmp(slot * 4);
-  RT_HIP(c, hipStreamSynchronize(c->stream));
+  int rc = join(c);
+  if (rc == RT_OK) rc = sync_all(c);
+  if (rc != RT_OK) return rc;
   for (int f = 0; f < F; ++f) {
     struct { const float* src; float4* dst; } items[3] = {
-        {pixels, c->pix[c->pix_slot[f]]}, {normals, c->nrm[f]}, {depth, c->dep[f]}};
+        {pixels, c->pix[c->pix_slot[f]]}, {normals, c->nrm[c->nrm_slot[f]]}, {depth, c->dep[c->dep_slot[f]]}};
     for (auto& it : items) {
       if (!it.src) continue;
       RT_HIP(c, hipMemcpy(tmp.data(), it.dst, slot * 16, hipMemcpyDeviceToHost));  // keep halo rows
@@ -581,6 +707,8 @@ int rt_reset_stats(rt_ctx* c) {
 int rt_enable_counters(rt_ctx* c, int on) {
   if (!c) return RT_E_INVAL;
   RT_HIP(c, hipSetDevice(c->device));
+  int jr = join(c);
+  if (jr != RT_OK) return jr;
   if (on && !c->d_counters) {
     RT_HIP(c, hipMalloc(&c->d_counters, rt::kCounters * rt::kCounterSlots * sizeof(unsigned long long)));
     RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kCounters * rt::kCounterSlots * sizeof(unsigned long long),
@@ -601,7 +729,8 @@ int rt_read_counters(rt_ctx* c, uint64_t out[8], int reset) {
   }
   RT_HIP(c, hipSetDevice(c->device));
   std::vector<unsigned long long> h((size_t)rt::kCounters * rt::kCounterSlots);
-  RT_HIP(c, hipStreamSynchronize(c->stream));
+  int rc = sync_all(c);
+  if (rc != RT_OK) return rc;
   RT_HIP(c, hipMemcpy(h.data(), c->d_counters, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   for (int k = 0; k < rt::kCounters; ++k) {
     unsigned long long sum = 0;
@@ -621,7 +750,8 @@ int rt_read_row_counters(rt_ctx* c, uint64_t* rows, int reset) {
   }
   RT_HIP(c, hipSetDevice(c->device));
   std::vector<unsigned long long> h(c->band_rows);
-  RT_HIP(c, hipStreamSynchronize(c->stream));
+  int rc = sync_all(c);
+  if (rc != RT_OK) return rc;
   RT_HIP(c, hipMemcpy(h.data(), c->d_row_counters, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   for (int k = 0; k < R; ++k) rows[k] = (uint64_t)h[(size_t)(c->own0 - c->band0) + k];
   if (reset) RT_HIP(c, hipMemset(c->d_row_counters, 0, h.size() * sizeof(unsigned long long)));

@@ -211,6 +211,15 @@ class Renderer:
         ptr = int(getattr(stream, "cuda_stream", stream))
         self._c(self._lib.rt_set_stream(self.ctx, C.c_void_p(ptr)), "rt_set_stream")
 
+    def enable_pipelining(self, on: bool = True, output_stream=None):
+        """Pipelined mode 1: frame k's post-process runs on `output_stream` (a torch.cuda.Stream
+        or an int hipStream_t; None = a stream of the context's own) while frame k+1's AO pass
+        runs on the main stream.  Bit-identical results; consumers of the image order their
+        work on the output stream (or synchronize)."""
+        ptr = None if output_stream is None else int(getattr(output_stream, "cuda_stream", output_stream))
+        self._c(self._lib.rt_enable_pipelining(self.ctx, int(bool(on)), C.c_void_p(ptr) if ptr is not None else None),
+                "rt_enable_pipelining")
+
     def synchronize(self):
         self._c(self._lib.rt_synchronize(self.ctx), "rt_synchronize")
 
