@@ -1,8 +1,10 @@
 #!/usr/bin/env python
 """Summarise a rocprofv3 kernel trace of `bench.py --warmup W --steps K` for profiles/:
 per-launch durations of the renderer's kernels in dispatch order and the mean over the timed
-launches (W warm-up first, then K timed, then the 2 counted frames), to compare with the
-bench line's live HIP-event kernel_ms.
+launches (W warm-up first, then K timed, then 2 standalone frames (not overlapped), then the 2
+counted frames), to compare with the bench line's live HIP-event kernel_ms and
+kernel_ms_standalone.  In pipelined mode 1 the timed post-process launches overlap the next
+frame's AO pass, so their spans are not kernel durations; the standalone ones are.
 
     python tools/trace_summary.py gpurun_out/<tag>/kt/run_kernel_trace.csv 8 10 "<command>"
 """
@@ -24,7 +26,8 @@ def main():
                                                          row["SGPR_Count"], row["LDS_Block_Size"]))
     if cmd:
         print(cmd)
-    print(f"per-launch durations (ms), in dispatch order: {warm} warm-up, {steps} timed, 2 counted (work counters on)")
+    print(f"per-launch durations (ms), in dispatch order: {warm} warm-up, {steps} timed, 2 standalone, "
+          f"2 counted (work counters on)")
     for key, ls in launches.items():
         ls.sort()
         ds = [d for _, d, *_ in ls]
@@ -33,6 +36,9 @@ def main():
         print(f"  all={[round(d, 3) for d in ds]}")
         if timed:
             print(f"  timed mean={sum(timed) / len(timed):.4f} ms")
+        solo = ds[warm + steps:warm + steps + 2]
+        if solo:
+            print(f"  standalone mean={sum(solo) / len(solo):.4f} ms")
 
 
 if __name__ == "__main__":
