@@ -118,3 +118,24 @@ def test_create_without_gpu_reports_nodev(gpu_available):
     ctx = C.c_void_p()
     assert lib.rt_create(0, C.byref(cfg), C.byref(ctx)) == _lib.RT_E_NODEV
     assert lib.rt_strerror(_lib.RT_E_NODEV) == b"no HIP device"
+
+
+def _headless():
+    import subprocess
+
+    exe = ROOT / "build" / "rt_headless"
+    if not exe.exists():
+        subprocess.run(["make", "-C", str(ROOT), "headless"], check=True, capture_output=True)
+    return exe
+
+
+def test_c_driver_links_against_the_abi(gpu_available):
+    """build/rt_headless is plain C++ over include/rt/abi.h + librtrt.so (the reference's own
+    render loop without GL): it links and runs; without a GPU rt_create reports NODEV."""
+    import subprocess
+
+    if gpu_available:
+        pytest.skip("covered by the GPU run")
+    p = subprocess.run([str(_headless()), "--width", "64", "--height", "48", "--frames", "2"],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 1 and "no HIP device" in p.stderr, (p.returncode, p.stderr)

@@ -42,3 +42,24 @@ def test_render_into_torch_tensor_on_torch_stream(side_stream):
         np.testing.assert_array_equal(got.view(np.uint32), r2.image().view(np.uint32))
         r.close()
         r2.close()
+
+
+@pytest.mark.parametrize("pipeline", ["0", "1"])
+def test_c_headless_driver_renders(tmp_path, pipeline):
+    """The C++ frame driver over the C ABI (the reference's render loop without GL): several
+    mode-1 frames, then the PPM image in place of the GL blit."""
+    import subprocess
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    exe = root / "build" / "rt_headless"
+    if not exe.exists():
+        subprocess.run(["make", "-C", str(root), "headless"], check=True, capture_output=True)
+    out = tmp_path / "frame.ppm"
+    p = subprocess.run([str(exe), "--width", "160", "--height", "120", "--frames", "10", "--mode", "1",
+                        "--pipeline", pipeline, "--ppm", str(out)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    assert "ms/frame" in p.stdout
+    data = out.read_bytes()
+    assert data.startswith(b"P6\n160 120\n255\n") and len(data) == len(b"P6\n160 120\n255\n") + 160 * 120 * 3
+    assert len(set(data[16:])) > 8  # not a blank frame
