@@ -83,7 +83,16 @@ def cpu_baseline(cfg_name: str, target_s: float) -> dict:
     rows = [int((i + 0.5) * H / n) for i in range(n)]
     t = run_rows(rows)
     units = len(rows) * W * (spp if mode in (1, 2) else 1)
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {"value": round(units / t / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "cpu": model,
             "sample": f"{len(rows)} of {H} rows (evenly spread) x {W} px x {spp if mode in (1, 2) else 1} spp, "
                       f"{'+'.join({1: 'aop_compute', 2: 'aop_postprocessing', 3: 'ao_compute', 4: 'p_compute', 5: 'h_compute'}[p] for p in progs)}, "
                       f"oracle/rt_oracle.c with {threads} OpenMP threads, {t:.1f} s; ms/frame extrapolated "
