@@ -358,7 +358,8 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4*
 // never accepted) and is skipped.
 // ---------------------------------------------------------------------------------------
 constexpr int kPool = 256;
-constexpr int kSetupCost = 24;  // per-sample setup (hashes, directions, shading) in sphere-test units
+constexpr int kSetupCost = 24;
+constexpr int kTailMaxObj = 128;  // split tail rounds stage the sphere table in LDS up to this size  // per-sample setup (hashes, directions, shading) in sphere-test units
 
 // Float form of the same cull (no trig): cone axis a, cos/sin of the half-angle; a sphere
 // with inflated radius r_eff (r_eff^2 = r^2 + 1e-5 (d^2 + r^2)) lies outside the forward and
@@ -421,7 +422,7 @@ __device__ inline bool cone_misses_f(const ConeF& c, float4 g, float cx, float c
 // handed to idle lanes by ds_bpermute whenever lanes run out of work.  Bounce rounds then
 // run with (nearly) all lanes live, and no per-sample setup runs at partial utilisation.
 // ---------------------------------------------------------------------------------------
-template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0>
+template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   extern __shared__ float4 lds[];
   const int spp = P.spp, W = P.W, D = P.D, nobj = P.nobj;
@@ -438,6 +439,11 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   float4* rls = (float4*)(((uintptr_t)(cmask + ((nobj + 63) >> 6)) + 15) & ~(uintptr_t)15);
   for (int k = lane; k < 2 * spp; k += 64) rls[k] = P.rb[k];
   for (int k = lane; k < TP; k += 64) pstop[k] = -1;
+  // TAIL: the sphere table in LDS (per-lane sphere indices in the split tail rounds)
+  float4* geol = rls + 2 * spp;  // [nobj] when TAIL && nobj <= kTailMaxObj
+  const bool tail_ok = TAIL && nobj <= kTailMaxObj;
+  if (tail_ok)
+    for (int k = lane; k < nobj; k += 64) geol[k] = geo[k];
   const float4* col = P.shapes + 2 * P.S;
   const float4* aux = P.shapes + 3 * P.S;
 
@@ -692,9 +698,49 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       }
       cursor += take;
     }
-    if (__ballot(has) == 0) break;
+    const unsigned long long hm = __ballot(has);
+    if (hm == 0) break;
     lap(2);
     if (ABL == 3) tsec[5] += 1;
+    // ---- split tail round: the pool has no fresh samples left and at most 32 paths are live.
+    // Each live path gets a group of G = 64/2^ceil(log2 L) lanes; lane p of the group tests
+    // spheres p, p+G, ... (ascending), and the group merges the partial results: minimum t,
+    // lowest index on ties = exactly the sequential scan's result (ao_compute.glsl:183-194).
+    const int L = __popcll(hm);
+    if (tail_ok && next >= total && cursor >= nlive && L <= 32) {
+      int c = 0;
+      while ((1 << c) < L) ++c;
+      const int G = 64 >> c;  // the largest power of 2 with G * L <= 64
+      const int rk = __builtin_amdgcn_mbcnt_hi((unsigned)(hm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)hm, 0u));
+      if (has) perm[rk] = lane;
+      __syncthreads();
+      const int g = lane / G, pl = lane - g * G;
+      const bool act = g < L;
+      const int owner = act ? perm[g] : lane;
+      const f3 o = mk(__shfl(pos.x, owner), __shfl(pos.y, owner), __shfl(pos.z, owner));
+      const f3 d = mk(__shfl(dir.x, owner), __shfl(dir.y, owner), __shfl(dir.z, owner));
+      float t = -1.0f;
+      int ind = -1;
+      if (act)
+        for (int i = pl; i < nobj; i += G) sphere_candidate(o, d, geol[i], i, 0.0001f, t, ind);
+      for (int m = 1; m < G; m <<= 1) {
+        const float tb = __shfl_xor(t, m);
+        const int ib = __shfl_xor(ind, m);
+        const bool take = ib >= 0 && (ind < 0 || tb < t || (tb == t && ib < ind));
+        t = take ? tb : t;
+        ind = take ? ib : ind;
+      }
+      const float tt = __shfl(t, rk * G);
+      const int ii = __shfl(ind, rk * G);
+      exec_tests += (unsigned long long)((nobj + G - 1) / G);
+      if (has) {
+        ++nseg;
+        has = shade(ii, tt, pos, dir, hemi, rr, rg, rb, depth, item, false);
+        depth -= 1;
+      }
+      lap(3);
+      continue;
+    }
     // ---- one bounce segment for every live path, against every sphere ------------------
     exec_tests += (unsigned long long)nobj;
     if (has) {
@@ -1269,20 +1315,24 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
     const long long grid = (npix + ppb - 1) / ppb;
     const size_t sh = lds + (size_t)block * sizeof(float4);
     // RTRT_AO_VARIANT: internal A/B switch for kernel experiments (tools/ab.py).
-    // Default 7: the pooled, batch-prepared kernel for all-sphere scenes.  11: without the
+    // Default 7: the pooled, batch-prepared kernel for all-sphere scenes, with split tail
+    // rounds when the sphere table fits in LDS.  17: without split tail rounds.  11: without the
     // lazy shortcuts.  20/25: the streaming sub-pool kernel (7 / 6 waves).  91-93: timing
     // ablations (bounce tests twice, culled primary tests twice, section clocks).  0/2: the
     // lane-per-sample kernel (the general one, used for scenes with planes).
     const char* ev = getenv("RTRT_AO_VARIANT");
     const int variant = ev ? atoi(ev) : 7;
-    if (all_spheres && (variant == 7 || variant == 11 || (variant >= 91 && variant <= 93))) {
+    if (all_spheres && (variant == 7 || variant == 17 || variant == 11 || (variant >= 91 && variant <= 93))) {
       const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
       const long long pools = (npix + TP - 1) / TP;
       const size_t psh = (size_t)TP * sizeof(float4) + (size_t)3 * TP * p.spp * sizeof(float) + (size_t)TP * sizeof(int) +
                          (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8 +
-                         16 + (size_t)2 * p.spp * sizeof(float4);
+                         16 + (size_t)2 * p.spp * sizeof(float4) +
+                         (variant == 7 && p.nobj <= kTailMaxObj ? (size_t)p.nobj * sizeof(float4) : 0);
       const dim3 g((unsigned)pools), b(64);
-      if (variant == 11)
+      if (variant == 7 && p.nobj <= kTailMaxObj)  // split tail rounds (the sphere table fits in LDS)
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true>), g, b, psh, stream, p, p.shapes);
+      else if (variant == 11)
         hipLaunchKernelGGL((ao_batch_kernel<7, false>), g, b, psh, stream, p, p.shapes);
       else if (variant == 91)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 1>), g, b, psh, stream, p, p.shapes);
@@ -1290,7 +1340,7 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2>), g, b, psh, stream, p, p.shapes);
       else if (variant == 93)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3>), g, b, psh, stream, p, p.shapes);
-      else
+      else  // 7 with a large scene, or 17: without the split tail rounds (A/B)
         hipLaunchKernelGGL(ao_batch_kernel<7>, g, b, psh, stream, p, p.shapes);
     } else if (all_spheres && (variant == 20 || variant == 25)) {
       constexpr int kSub = 128, kRing = 2, kWaveSub = 8;  // sub-pool samples, ring slots, sub-pools per wave
