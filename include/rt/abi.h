@@ -85,13 +85,14 @@ int rt_set_stream(rt_ctx* ctx, void* hip_stream);
 /* Go back to the context's own (non-blocking) stream. */
 int rt_use_own_stream(rt_ctx* ctx);
 void* rt_get_stream(rt_ctx* ctx);
-/* Pipelined mode 1 (on != 0): rt_dispatch(RT_MODE_AO_PP) runs frame k's post-process
- * (aop_postprocessing) on `output_stream` (NULL: a stream of the context's own) while frame
- * k+1's aop_compute runs on the main stream.  Results are bit-identical to the sequential
- * order (the ring's normals/depth/raw pixels rotate through spare buffers, so the overlap
- * has no hazard).  The image of a pipelined frame is complete in output-stream order;
- * rt_synchronize, rt_download and every other call (which first orders the output stream
- * before the main stream) see finished frames.  Off by default. */
+/* Pipelined mode 1 (on != 0): rt_dispatch(RT_MODE_AO_PP) runs consecutive frames' aop_compute
+ * passes on two alternating streams (the main stream and one of the context's own), so frame
+ * k+1's pass fills the tail of frame k's, and every aop_postprocessing pass on `output_stream`
+ * (NULL: a stream of the context's own).  Results are bit-identical to the sequential order:
+ * normals/depth/raw pixels rotate through spare buffers and the header has two device copies,
+ * so no pass sees data another in-flight pass writes.  A pipelined frame's image is complete in
+ * output-stream order; rt_synchronize, rt_download and every other call (each first orders
+ * all streams before the main stream) see finished frames.  Off by default. */
 int rt_enable_pipelining(rt_ctx* ctx, int on, void* output_stream);
 void* rt_get_output_stream(rt_ctx* ctx);
 /* Wait for all of the context's work (both streams). */

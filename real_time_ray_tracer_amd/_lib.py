@@ -99,6 +99,15 @@ def load() -> C.CDLL:
     if not path.exists():
         raise RuntimeError(f"{path} not found: the HIP library is required (build it with `make lib` "
                            f"or __graft_entry__.build()); there is no CPU fallback")
+    # One HIP runtime per process: PyTorch bundles its own libamdhip64 (same soname as
+    # /opt/rocm's).  Whichever loads first serves both, and torch cannot start on the other
+    # one, while torch streams handed to rt_set_stream must belong to the runtime the library
+    # uses.  So when torch is installed it is imported (and its runtime loaded) first.
+    if os.environ.get("RTRT_NO_TORCH_FIRST") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     lib = C.CDLL(str(path))
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -11,12 +11,15 @@
 // reference's 2 x 55.76 MB host round trip per frame.  The reference [F][W][H] layout is
 // produced only by rt_download / consumed by rt_upload_gbuffer.
 //
-// Pipelined mode 1 (rt_enable_pipelining): frame k's post-process runs on a second stream
-// while frame k+1's AO pass runs.  AO k+1 writes its normals/depth into the spare buffers and
-// its raw pixels into one of the two spare pixel buffers, so the post-process of frame k,
-// which may read slot (k+1)%8's previous contents as its oldest history, never sees them
-// change; AO k waits for post k-2 (the last reader of the buffers it overwrites).  The
-// results are those of the sequential order, bit for bit.
+// Pipelined mode 1 (rt_enable_pipelining): consecutive frames' AO passes run on two
+// alternating streams (so frame k+1's AO fills the tail of frame k's), and every post-process
+// runs on a third, output stream.  AO k writes its normals/depth into free buffers (a queue of
+// two) and its raw pixels into one of the two spare pixel buffers, and reads its header from
+// its own copy (two copies), so nothing another in-flight pass reads changes under it: the
+// post-process of frame k-1 may read slot k%8's previous contents as its oldest history, and
+// AO k itself reads them for the stale normal/depth of emissive first hits.  AO k waits for
+// post k-2 (the last reader of the buffers it overwrites); post k waits for AO k.  The results
+// are those of the sequential order, bit for bit.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,6 +39,12 @@ constexpr int kMaxShapes = 2048;
 constexpr int kMaxSpp = 256;
 constexpr int kMaxDepth = 65535;  // stop values are packed in 16 bits by the pooled AO kernel
 constexpr int kStageSlots = 8;
+// Pipelining depth D: AO k waits for post k-D, the last reader of the raw pixel buffer and the
+// normals/depth buffers it overwrites (D of each rotate outside the slot map)
+constexpr int kPipe = 4;  // capacity; the depth in use is rt_ctx::pipe_depth (default 3)
+// AO streams: pipelined frame k's AO pass runs on AO stream k % n_ao_streams (0 = the main
+// stream) and reads header copy k % n_ao_streams
+constexpr int kAoStreams = 3;  // capacity; in use: rt_ctx::n_ao_streams (default 2)
 
 struct Stage {
   void* host = nullptr;  // pinned
@@ -53,19 +62,24 @@ struct rt_ctx {
   int band0 = 0, band_rows = 0;  // strip + 1-row halo (post-process neighbours)
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  float4* d_shapes = nullptr;  // [4][S]
-  float4* d_rb = nullptr;      // [2*spp]
-  std::vector<float4*> pix;    // F+2 buffers
+  float4* d_shapes_buf[kAoStreams] = {};  // [4][S], one copy per AO stream
+  float4* d_rb_buf[kAoStreams] = {};      // [2*spp]
+  float4* d_shapes = nullptr;  // the copy the next dispatch reads
+  float4* d_rb = nullptr;
+  std::vector<float4*> pix;    // F+pipe_depth buffers
   std::vector<int> pix_slot;   // slot -> buffer index
-  int spare = 0, spare2 = 0;   // pixel buffers outside the map
-  std::vector<float4*> nrm, dep;       // F+1 buffers each
+  int spare = 0;               // pixel buffer outside the map (sequential post-process target)
+  int raw_buf[kPipe] = {};     // raw_buf[1..]: more pixel buffers outside the map (pipelined raw AO output)
+  std::vector<float4*> nrm, dep;       // F+pipe_depth buffers each
   std::vector<int> nrm_slot, dep_slot;  // slot -> buffer index
-  int nrm_spare = 0, dep_spare = 0;
+  int nrm_free[kPipe] = {}, dep_free[kPipe] = {};  // buffers outside the map, oldest first
   // pipelined mode 1
   bool pipelined = false;
   hipStream_t out_stream = nullptr, own_out_stream = nullptr;
-  hipEvent_t ev_ao = nullptr, ev_post[2] = {nullptr, nullptr}, ev_join = nullptr;
-  bool post_recorded[2] = {false, false};
+  hipStream_t ao_streams[kAoStreams] = {};  // [0] unused (the main stream); [1..] the context's own
+  int pipe_depth = 3, n_ao_streams = 2;
+  hipEvent_t ev_ao = nullptr, ev_post[kPipe] = {}, ev_join = nullptr, ev_seq = nullptr;
+  bool post_recorded[kPipe] = {};
   long long pipe_n = 0;
   bool out_pending = false;
   float4* d_image_own = nullptr;
@@ -118,7 +132,7 @@ hipEvent_t get_event(rt_ctx* c) {
 
 // Async H2D copy through a ring of pinned staging buffers, so callers may reuse their
 // (pageable) memory as soon as the call returns and the stream never has to drain.
-int staged_copy(rt_ctx* c, void* dst, const void* src, size_t bytes) {
+int staged_copy(rt_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
   if (bytes == 0) return RT_OK;
   Stage& s = c->stage[c->stage_next];
   c->stage_next = (c->stage_next + 1) % kStageSlots;
@@ -131,8 +145,8 @@ int staged_copy(rt_ctx* c, void* dst, const void* src, size_t bytes) {
   }
   if (!s.done) RT_HIP(c, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
   std::memcpy(s.host, src, bytes);
-  RT_HIP(c, hipMemcpyAsync(dst, s.host, bytes, hipMemcpyHostToDevice, c->stream));
-  RT_HIP(c, hipEventRecord(s.done, c->stream));
+  RT_HIP(c, hipMemcpyAsync(dst, s.host, bytes, hipMemcpyHostToDevice, st));
+  RT_HIP(c, hipEventRecord(s.done, st));
   s.used = true;
   return RT_OK;
 }
@@ -152,13 +166,19 @@ void free_all(rt_ctx* c) {
   for (auto p : c->nrm) if (p) (void)hipFree(p);
   for (auto p : c->dep) if (p) (void)hipFree(p);
   if (c->d_image_own) (void)hipFree(c->d_image_own);
-  if (c->d_shapes) (void)hipFree(c->d_shapes);
-  if (c->d_rb) (void)hipFree(c->d_rb);
+  for (int k = 0; k < kAoStreams; ++k) {
+    if (c->d_shapes_buf[k]) (void)hipFree(c->d_shapes_buf[k]);
+    if (c->d_rb_buf[k]) (void)hipFree(c->d_rb_buf[k]);
+  }
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->d_row_counters) (void)hipFree(c->d_row_counters);
-  for (auto e : {c->ev_ao, c->ev_post[0], c->ev_post[1], c->ev_join})
+  for (auto e : {c->ev_ao, c->ev_join, c->ev_seq})
+    if (e) (void)hipEventDestroy(e);
+  for (auto e : c->ev_post)
     if (e) (void)hipEventDestroy(e);
   if (c->own_out_stream) (void)hipStreamDestroy(c->own_out_stream);
+  for (int k = 1; k < kAoStreams; ++k)
+    if (c->ao_streams[k]) (void)hipStreamDestroy(c->ao_streams[k]);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
 }
 
@@ -166,17 +186,34 @@ void free_all(rt_ctx* c) {
 // (every call except a pipelined mode-1 dispatch starts with this).
 int join(rt_ctx* c) {
   if (!c->out_pending) return RT_OK;
+  for (int k = 1; k < c->n_ao_streams; ++k) {
+    RT_HIP(c, hipEventRecord(c->ev_join, c->ao_streams[k]));
+    RT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+  }
   RT_HIP(c, hipEventRecord(c->ev_join, c->out_stream));
   RT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
   c->out_pending = false;
-  c->post_recorded[0] = c->post_recorded[1] = false;  // ordered by the join from now on
+  for (auto& r : c->post_recorded) r = false;  // ordered by the join from now on
   c->pipe_n = 0;
   return RT_OK;
 }
 
 int sync_all(rt_ctx* c) {
   RT_HIP(c, hipStreamSynchronize(c->stream));
+  for (int k = 1; k < kAoStreams; ++k)
+    if (c->ao_streams[k]) RT_HIP(c, hipStreamSynchronize(c->ao_streams[k]));
   if (c->out_stream && c->out_stream != c->stream) RT_HIP(c, hipStreamSynchronize(c->out_stream));
+  return RT_OK;
+}
+
+// Stream and header copy of the next header upload / AO pass: pipelined frames alternate
+// between the main stream + copy 0 and the second stream + copy 1.
+int hdr_copy(const rt_ctx* c) { return c->pipelined ? (int)(c->pipe_n % c->n_ao_streams) : 0; }
+hipStream_t ao_stream(const rt_ctx* c) { return hdr_copy(c) ? c->ao_streams[hdr_copy(c)] : c->stream; }
+// a new pipelined sequence: the other AO streams start after everything issued so far
+int start_sequence(rt_ctx* c) {
+  RT_HIP(c, hipEventRecord(c->ev_seq, c->stream));
+  for (int k = 1; k < c->n_ao_streams; ++k) RT_HIP(c, hipStreamWaitEvent(c->ao_streams[k], c->ev_seq, 0));
   return RT_OK;
 }
 
@@ -282,30 +319,46 @@ int run_program(rt_ctx* c, int program, int frame) {
   }
 }
 
-// One pipelined mode-1 frame (see the header comment): AO on the main stream into fresh
-// normals/depth and a raw pixel buffer, post-process on the output stream.
+// One pipelined mode-1 frame (see the header comment): AO on the frame's AO stream into free
+// normals/depth buffers and a raw pixel buffer, post-process on the output stream.
 int pipelined_frame(rt_ctx* c, int frame) {
   if (!c->have_header) return RT_E_STATE;
   if (frame < 0 || frame >= c->cfg.num_frames) return RT_E_INVAL;
   RT_HIP(c, hipSetDevice(c->device));
-  const int n2 = (int)(c->pipe_n & 1);
-  if (c->post_recorded[n2]) RT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_post[n2], 0));  // post k-2
-  float4* raw = c->pix[n2 ? c->spare2 : c->spare];
+  const int D = c->pipe_depth;
+  const int nq = (int)(c->pipe_n % D);
+  hipStream_t st = ao_stream(c);
+  if (c->pipe_n == 0) {  // a new sequence: the other AO streams start after everything so far
+    int sr = start_sequence(c);
+    if (sr != RT_OK) return sr;
+  }
+  if (c->post_recorded[nq]) RT_HIP(c, hipStreamWaitEvent(st, c->ev_post[nq], 0));  // post k-D
+  float4* raw = c->pix[nq == 0 ? c->spare : c->raw_buf[nq]];  // the sequential spare is raw buffer 0
   rt::FrameParams p;
   fill_params(c, frame, p);
+  p.shapes = c->d_shapes_buf[hdr_copy(c)];
+  p.rb = c->d_rb_buf[hdr_copy(c)];
   p.trace_row0 = c->band0;
   p.trace_rows = c->band_rows;
   p.out_pix = raw;
   p.image = nullptr;
   p.nrm_prev = p.nrm;  // the slot's previous contents (stale reads)
   p.dep_prev = p.dep;
-  p.nrm = c->nrm[c->nrm_spare];
-  p.dep = c->dep[c->dep_spare];
-  int rc = launch(c, RT_PROG_AOP_COMPUTE, p, c->stream);
+  const int xn = c->nrm_free[0], xd = c->dep_free[0];
+  p.nrm = c->nrm[xn];
+  p.dep = c->dep[xd];
+  int rc = launch(c, RT_PROG_AOP_COMPUTE, p, st);
   if (rc != RT_OK) return rc;
-  std::swap(c->nrm_slot[frame], c->nrm_spare);
-  std::swap(c->dep_slot[frame], c->dep_spare);
-  RT_HIP(c, hipEventRecord(c->ev_ao, c->stream));
+  // the slot now maps to the fresh buffers; its previous ones join the back of the free queue
+  for (int q = 0; q + 1 < D; ++q) {
+    c->nrm_free[q] = c->nrm_free[q + 1];
+    c->dep_free[q] = c->dep_free[q + 1];
+  }
+  c->nrm_free[D - 1] = c->nrm_slot[frame];
+  c->dep_free[D - 1] = c->dep_slot[frame];
+  c->nrm_slot[frame] = xn;
+  c->dep_slot[frame] = xd;
+  RT_HIP(c, hipEventRecord(c->ev_ao, st));
   RT_HIP(c, hipStreamWaitEvent(c->out_stream, c->ev_ao, 0));
   rt::FrameParams q;
   fill_params(c, frame, q);
@@ -315,10 +368,12 @@ int pipelined_frame(rt_ctx* c, int frame) {
   q.out_pix = c->pix[c->pix_slot[frame]];  // filtered in place of slot `frame`'s oldest contents
   rc = launch(c, RT_PROG_AOP_POSTPROCESSING, q, c->out_stream);
   if (rc != RT_OK) return rc;
-  RT_HIP(c, hipEventRecord(c->ev_post[n2], c->out_stream));
-  c->post_recorded[n2] = true;
+  RT_HIP(c, hipEventRecord(c->ev_post[nq], c->out_stream));
+  c->post_recorded[nq] = true;
   c->out_pending = true;
   c->pipe_n += 1;
+  c->d_shapes = c->d_shapes_buf[hdr_copy(c)];  // what a sequential dispatch would read next
+  c->d_rb = c->d_rb_buf[hdr_copy(c)];
   return RT_OK;
 }
 
@@ -392,6 +447,9 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
   if (!x) return RT_E_NOMEM;
   x->device = device;
   x->cfg = c;
+  // pipelining shape (A/B knobs): RTRT_PIPE_DEPTH in [2, kPipe], RTRT_AO_STREAMS in [1, kAoStreams]
+  if (const char* ev = getenv("RTRT_PIPE_DEPTH")) x->pipe_depth = std::min(kPipe, std::max(2, atoi(ev)));
+  if (const char* ev = getenv("RTRT_AO_STREAMS")) x->n_ao_streams = std::min(kAoStreams, std::max(1, atoi(ev)));
   x->own0 = c.row_begin;
   x->own_rows = c.row_end - c.row_begin;
   x->band0 = std::max(0, c.row_begin - 1);
@@ -407,23 +465,28 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
   const size_t slot = slot_elems(x) * sizeof(float4);
   const int F = c.num_frames;
   if (e == hipSuccess) {
-    x->pix.assign(F + 2, nullptr);
-    x->nrm.assign(F + 1, nullptr);
-    x->dep.assign(F + 1, nullptr);
-    for (int k = 0; k < F + 2 && e == hipSuccess; ++k) e = hipMalloc(&x->pix[k], slot);
-    for (int k = 0; k < F + 1 && e == hipSuccess; ++k) e = hipMalloc(&x->nrm[k], slot);
-    for (int k = 0; k < F + 1 && e == hipSuccess; ++k) e = hipMalloc(&x->dep[k], slot);
+    const int NB = F + x->pipe_depth;
+    x->pix.assign(NB, nullptr);
+    x->nrm.assign(NB, nullptr);
+    x->dep.assign(NB, nullptr);
+    for (int k = 0; k < NB && e == hipSuccess; ++k) e = hipMalloc(&x->pix[k], slot);
+    for (int k = 0; k < NB && e == hipSuccess; ++k) e = hipMalloc(&x->nrm[k], slot);
+    for (int k = 0; k < NB && e == hipSuccess; ++k) e = hipMalloc(&x->dep[k], slot);
     // value-initialised ssbo_CPUMEM: the ring starts at zero
-    for (int k = 0; k < F + 2 && e == hipSuccess; ++k) e = hipMemsetAsync(x->pix[k], 0, slot, x->stream);
-    for (int k = 0; k < F + 1 && e == hipSuccess; ++k) e = hipMemsetAsync(x->nrm[k], 0, slot, x->stream);
-    for (int k = 0; k < F + 1 && e == hipSuccess; ++k) e = hipMemsetAsync(x->dep[k], 0, slot, x->stream);
-    for (hipEvent_t* ev : {&x->ev_ao, &x->ev_post[0], &x->ev_post[1], &x->ev_join})
+    for (int k = 0; k < NB && e == hipSuccess; ++k) e = hipMemsetAsync(x->pix[k], 0, slot, x->stream);
+    for (int k = 0; k < NB && e == hipSuccess; ++k) e = hipMemsetAsync(x->nrm[k], 0, slot, x->stream);
+    for (int k = 0; k < NB && e == hipSuccess; ++k) e = hipMemsetAsync(x->dep[k], 0, slot, x->stream);
+    for (hipEvent_t* ev : {&x->ev_ao, &x->ev_join, &x->ev_seq})
       if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    for (auto& ev : x->ev_post)
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipMalloc(&x->d_image_own, (size_t)x->own_rows * c.width * sizeof(float4));
   if (e == hipSuccess) e = hipMemsetAsync(x->d_image_own, 0, (size_t)x->own_rows * c.width * sizeof(float4), x->stream);
-  if (e == hipSuccess) e = hipMalloc(&x->d_shapes, (size_t)4 * std::max(1, c.num_shapes) * sizeof(float4));
-  if (e == hipSuccess) e = hipMalloc(&x->d_rb, (size_t)2 * c.spp * sizeof(float4));
+  for (int k = 0; k < kAoStreams; ++k) {
+    if (e == hipSuccess) e = hipMalloc(&x->d_shapes_buf[k], (size_t)4 * std::max(1, c.num_shapes) * sizeof(float4));
+    if (e == hipSuccess) e = hipMalloc(&x->d_rb_buf[k], (size_t)2 * c.spp * sizeof(float4));
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(x->stream);
   if (e != hipSuccess) {
     fail(e);
@@ -437,8 +500,12 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
   x->dep_slot.resize(F);
   for (int k = 0; k < F; ++k) x->pix_slot[k] = x->nrm_slot[k] = x->dep_slot[k] = k;
   x->spare = F;
-  x->spare2 = F + 1;
-  x->nrm_spare = x->dep_spare = F;
+  for (int q = 0; q < x->pipe_depth; ++q) {
+    x->raw_buf[q] = F + q;  // raw buffer 0 is whichever buffer is the sequential spare
+    x->nrm_free[q] = x->dep_free[q] = F + q;
+  }
+  x->d_shapes = x->d_shapes_buf[0];
+  x->d_rb = x->d_rb_buf[0];
   x->out_stream = x->own_stream;
   x->header.assign(rt_header_bytes(c.num_shapes, c.spp) / 4, 0.0f);
   x->table.assign((size_t)4 * std::max(1, c.num_shapes), make_float4(0, 0, 0, 0));
@@ -461,15 +528,23 @@ int rt_set_stream(rt_ctx* c, void* s) {
   int rc = sync_all(c);
   if (rc != RT_OK) return rc;
   c->out_pending = false;
-  c->post_recorded[0] = c->post_recorded[1] = false;
+  for (auto& r : c->post_recorded) r = false;
   c->pipe_n = 0;
   c->stream = (hipStream_t)s;  // NULL = the legacy NULL stream
   if (!c->pipelined) c->out_stream = c->stream;
+  // an idle own stream is released: every stream holds one of the process's few hardware
+  // queues (GPU_MAX_HW_QUEUES), and busy streams that share one serialise
+  if (c->own_stream && c->stream != c->own_stream && c->out_stream != c->own_stream) {
+    RT_HIP(c, hipStreamDestroy(c->own_stream));
+    c->own_stream = nullptr;
+  }
   return RT_OK;
 }
 
 int rt_use_own_stream(rt_ctx* c) {
   if (!c) return RT_E_INVAL;
+  RT_HIP(c, hipSetDevice(c->device));
+  if (!c->own_stream) RT_HIP(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
   return rt_set_stream(c, (void*)c->own_stream);
 }
 
@@ -479,13 +554,15 @@ int rt_enable_pipelining(rt_ctx* c, int on, void* output_stream) {
   int rc = sync_all(c);
   if (rc != RT_OK) return rc;
   c->out_pending = false;
-  c->post_recorded[0] = c->post_recorded[1] = false;
+  for (auto& r : c->post_recorded) r = false;
   c->pipe_n = 0;
   c->pipelined = on != 0;
   if (!c->pipelined) {
     c->out_stream = c->stream;
     return RT_OK;
   }
+  for (int k = 1; k < c->n_ao_streams; ++k)
+    if (!c->ao_streams[k]) RT_HIP(c, hipStreamCreateWithFlags(&c->ao_streams[k], hipStreamNonBlocking));
   if (output_stream) {
     c->out_stream = (hipStream_t)output_stream;
   } else {
@@ -532,10 +609,20 @@ int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
     if (i < nobj && id != RT_SHAPE_SPHERE) allsph = false;
   }
   RT_HIP(c, hipSetDevice(c->device));
-  int rc = staged_copy(c, c->d_shapes, c->table.data(), (size_t)4 * std::max(1, S) * sizeof(float4));
+  // pipelined: into the header copy of the next frame, on its AO stream (ordered after the AO
+  // pass two frames back that read that copy); sequential: in place, on the main stream
+  const int hc = hdr_copy(c);
+  if (c->pipelined && c->pipe_n == 0) {  // the first frame of a sequence: order after everything
+    int sr = start_sequence(c);
+    if (sr != RT_OK) return sr;
+  }
+  int rc = staged_copy(c, c->d_shapes_buf[hc], c->table.data(), (size_t)4 * std::max(1, S) * sizeof(float4),
+                       ao_stream(c));
   if (rc != RT_OK) return rc;
-  rc = staged_copy(c, c->d_rb, h + rt_off_rand(S) / 4, (size_t)2 * spp * sizeof(float4));
+  rc = staged_copy(c, c->d_rb_buf[hc], h + rt_off_rand(S) / 4, (size_t)2 * spp * sizeof(float4), ao_stream(c));
   if (rc != RT_OK) return rc;
+  c->d_shapes = c->d_shapes_buf[hc];
+  c->d_rb = c->d_rb_buf[hc];
   c->nobj = nobj;
   c->all_spheres = allsph;
   c->have_header = true;
@@ -546,7 +633,16 @@ int rt_upload_rand_buffer(rt_ctx* c, const float* rb, size_t n_vec4) {
   if (!c || !rb || n_vec4 != (size_t)2 * c->cfg.spp) return RT_E_INVAL;
   std::memcpy(c->header.data() + rt_off_rand(c->cfg.num_shapes) / 4, rb, n_vec4 * 16);
   RT_HIP(c, hipSetDevice(c->device));
-  return staged_copy(c, c->d_rb, rb, n_vec4 * 16);
+  const int hc = hdr_copy(c);
+  int rc = staged_copy(c, c->d_rb_buf[hc], rb, n_vec4 * 16, ao_stream(c));
+  if (rc != RT_OK) return rc;
+  // the other copy keeps the shape table: bring it along when switching copies
+  if (c->d_shapes != c->d_shapes_buf[hc])
+    RT_HIP(c, hipMemcpyAsync(c->d_shapes_buf[hc], c->d_shapes, (size_t)4 * std::max(1, c->cfg.num_shapes) * sizeof(float4),
+                             hipMemcpyDeviceToDevice, ao_stream(c)));
+  c->d_shapes = c->d_shapes_buf[hc];
+  c->d_rb = c->d_rb_buf[hc];
+  return RT_OK;
 }
 
 int rt_run_program(rt_ctx* c, int program, int frame) {
