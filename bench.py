@@ -25,6 +25,12 @@ from pathlib import Path
 
 import numpy as np
 
+# Pipelined frames keep three streams busy (two AO streams + the output stream) beside
+# RCCL's: with HIP's default of 4 hardware queues per process two of them can land on one
+# queue and serialise.  8 queues (must be set before the HIP runtime starts; <= 32).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
