@@ -608,16 +608,16 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       pool_xy(lp, x, y);
       const float px = (float)x, py = (float)y;
       float hp, vp;
-      if (aa == 0) {
-        hp = px / P.fW;
-        vp = py / P.fH;
-      } else {  // ao_compute.glsl:310-323
+      {  // ao_compute.glsl:310-323; sample 0 is unjittered: px + 0 == px, so one path for
+        // every lane (no divergent branch in the batch)
         float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
         float u = grandom(((s.x + px * f.z) - px) + f.x, ((f.y + py * s.w) - py) + s.y);
         float w = grandom(s.z * px - (f.x * px) * f.z, f.w * py - (s.y * py) * s.w);
         normalize2(u, w);
-        hp = (px + (u / 6.0f - 0.08333f)) / P.fW;
-        vp = (py + (w / 6.0f - 0.08333f)) / P.fH;
+        const float jx = aa == 0 ? 0.0f : u / 6.0f - 0.08333f;
+        const float jy = aa == 0 ? 0.0f : w / 6.0f - 0.08333f;
+        hp = (px + jx) / P.fW;
+        vp = (py + jy) / P.fH;
       }
       bdir = primary_dir(P, hp, vp);
       // get_pt_within_unit_sphere(aa), hoisted: it depends on aa and the pixel only, so it is
@@ -1047,16 +1047,16 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
       pool_xy(lp, x, y);
       const float px = (float)x, py = (float)y;
       float hp, vp;
-      if (aa == 0) {
-        hp = px / P.fW;
-        vp = py / P.fH;
-      } else {  // ao_compute.glsl:310-323
+      {  // ao_compute.glsl:310-323; sample 0 is unjittered: px + 0 == px, so one path for
+        // every lane (no divergent branch in the batch)
         float4 f = rbuf[2 * aa], sv = rbuf[2 * aa + 1];
         float u = grandom(((sv.x + px * f.z) - px) + f.x, ((f.y + py * sv.w) - py) + sv.y);
         float w = grandom(sv.z * px - (f.x * px) * f.z, f.w * py - (sv.y * py) * sv.w);
         normalize2(u, w);
-        hp = (px + (u / 6.0f - 0.08333f)) / P.fW;
-        vp = (py + (w / 6.0f - 0.08333f)) / P.fH;
+        const float jx = aa == 0 ? 0.0f : u / 6.0f - 0.08333f;
+        const float jy = aa == 0 ? 0.0f : w / 6.0f - 0.08333f;
+        hp = (px + jx) / P.fW;
+        vp = (py + jy) / P.fH;
       }
       bdir = primary_dir(P, hp, vp);
       bpos = cam;
