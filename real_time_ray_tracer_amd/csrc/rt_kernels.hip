@@ -94,33 +94,129 @@ __device__ __forceinline__ void store_color(const FrameParams& P, int x, int y, 
 }
 
 // ---------------------------------------------------------------------------------------
+// Primary-ray cone culling (used by ao_batch_kernel, phong_kernel, hybrid_kernel).  Every primary ray starts at the camera
+// and passes through the pool's pixel rectangle (jitter < 0.0834 px), so one cone bounds
+// them.  A sphere whose line distance from every ray of the cone exceeds its radius by a
+// float-error margin has a computed discriminant < 0 for every lane (-1 in the reference,
+// never accepted) and is skipped.
+// ---------------------------------------------------------------------------------------
+constexpr int kPool = 256;
+constexpr int kSetupCost = 24;
+constexpr int kTailMaxObj = 128;  // split tail rounds stage the sphere table in LDS up to this size  // per-sample setup (hashes, directions, shading) in sphere-test units
+
+// Float form of the same cull (no trig): cone axis a, cos/sin of the half-angle; a sphere
+// with inflated radius r_eff (r_eff^2 = r^2 + 1e-5 (d^2 + r^2)) lies outside the forward and
+// the backward cone iff |cos phi| < cos(theta + alpha), sin alpha = r_eff / d.  Float error
+// (~1e-6) is covered by the 2e-5 slack on the cosine and the 1e-5 inflation.
+struct ConeF {
+  float ax, ay, az, ct, st;
+};
+
+// The cone only has to be conservative, not bit-exact: it is built with the raw
+// v_rcp/v_sqrt/v_rsq instructions (<= 1 ulp, ~1e-7 relative), far inside the 2e-5 cosine
+// slack and the 1e-5 radius inflation.
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float fast_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
+
+__device__ inline ConeF pool_cone_f(const FrameParams& P, int xmin, int xmax, int ymin, int ymax) {
+  const float iw = fast_rcp(P.fW), ih = fast_rcp(P.fH);
+  const float hps[2] = {((float)xmin - 0.1f) * iw, ((float)xmax + 0.1f) * iw};
+  const float vps[2] = {((float)ymin - 0.1f) * ih, ((float)ymax + 0.1f) * ih};
+  f3 d[4];
+  f3 sum = mk(0.0f, 0.0f, 0.0f);
+  for (int k = 0; k < 4; ++k) {
+    float hp = hps[k & 1], vp = vps[k >> 1];
+    f3 v = mk(P.lx + hp * P.hx + vp * P.vx, P.ly + hp * P.hy + vp * P.vy, P.lz + hp * P.hz + vp * P.vz);
+    d[k] = fast_rsq(dot(v, v)) * v;
+    sum = sum + d[k];
+  }
+  const float il = fast_rsq(dot(sum, sum));
+  ConeF c;
+  c.ax = sum.x * il; c.ay = sum.y * il; c.az = sum.z * il;
+  float ct = 1.0f;
+  for (int k = 0; k < 4; ++k) ct = fminf(ct, c.ax * d[k].x + c.ay * d[k].y + c.az * d[k].z);
+  ct = fminf(fmaxf(ct - 2e-5f, -1.0f), 1.0f);  // widen the cone a little (direction rounding)
+  c.ct = ct;
+  c.st = fast_sqrt(fmaxf(0.0f, 1.0f - ct * ct));
+  return c;
+}
+
+__device__ inline bool cone_misses_f(const ConeF& c, float4 g, float cx, float cy, float cz) {
+  float Lx = g.x - cx, Ly = g.y - cy, Lz = g.z - cz;
+  float d2 = Lx * Lx + Ly * Ly + Lz * Lz, r2 = g.w * g.w;
+  float reff2 = r2 + 1e-5f * (d2 + r2);
+  if (!(d2 > reff2 * 1.01f + 1e-6f)) return false;  // camera inside / near the sphere: keep
+  float id = fast_rsq(d2);
+  float sa2 = reff2 * (id * id);
+  float sa = fast_sqrt(sa2), ca = fast_sqrt(fmaxf(0.0f, 1.0f - sa2));
+  float K = c.ct * ca - c.st * sa - 2e-5f;  // cos(theta + alpha), made smaller (conservative)
+  if (!(K > 0.0f)) return false;
+  float cphi = (c.ax * Lx + c.ay * Ly + c.az * Lz) * id;
+  return fabsf(cphi) < K;
+}
+
+// Closest hit of the camera rays of a pixel rectangle whose cone is `cone`: per 64-sphere
+// word the wave culls the spheres lane-parallel, then tests the survivors in ascending index
+// order, reading them on the scalar path (wave-uniform index).  Same result as closest_hit.
+__device__ __forceinline__ int closest_hit_cone(const float4* __restrict__ geo, int nobj, const ConeF& cone, f3 cam,
+                                                f3 dir, float thr, float& t_out) {
+  float t = -1.0f;
+  int ind = -1;
+  const int lane = threadIdx.x & 63;
+  for (int w = 0; w < nobj; w += 64) {
+    const int i = w + lane;
+    const bool keep = i < nobj && !cone_misses_f(cone, geo[i], cam.x, cam.y, cam.z);
+    unsigned long long m = __ballot(keep);
+    m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
+        (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
+    while (m) {
+      const int k = w + __builtin_ctzll(m);
+      m &= m - 1;
+      sphere_candidate(cam, dir, geo[k], k, thr, t, ind);
+    }
+  }
+  t_out = t;
+  return ind;
+}
+
+// The cone of the camera rays through this wave's 8x8 pixel tile (tile_xy).
+__device__ __forceinline__ ConeF wave_tile_cone(const FrameParams& P) {
+  const int wave = threadIdx.x >> 6;
+  const int x0 = blockIdx.x * 16 + (wave & 1) * 8, y0 = P.trace_row0 + blockIdx.y * 16 + (wave >> 1) * 8;
+  return pool_cone_f(P, x0, x0 + 7, y0, y0 + 7);
+}
+
+// ---------------------------------------------------------------------------------------
 // mode 3 — p_compute.glsl:168-245
 // ---------------------------------------------------------------------------------------
 template <bool ALLSPH>
 __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
+  // all-sphere scenes: the table is read on the scalar path from global memory and the
+  // primary rays of each wave's 8x8 tile are cone-culled; general scenes: LDS table
   extern __shared__ float4 lds[];
-  stage_shapes(P, lds);
-  __syncthreads();
+  if (!ALLSPH) {
+    stage_shapes(P, lds);
+    __syncthreads();
+  }
   const int n = P.nobj;
-  const float4 *geo = lds, *geo2 = lds + n, *col = lds + 2 * n;
+  const float4* geo = ALLSPH ? P.shapes : lds;
+  const float4 *geo2 = geo + (ALLSPH ? P.S : n), *col = geo + 2 * (ALLSPH ? P.S : n);
   int x, y;
   tile_xy(x, y, P.trace_row0);
   const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
-  if (P.counters || P.row_counters) {
-    unsigned hit = 0;
-    if (active) {
-      float t;
-      f3 d = primary_dir(P, (float)x / (float)P.W, (float)y / (float)P.H);
-      hit = closest_hit<ALLSPH>(geo, geo2, n, mk(P.cx, P.cy, P.cz), d, 0.0f, t) == -1 ? 0u : 1u;
-    }
-    count_work(P, active, y, 1u, hit);
-  }
-  if (!active) return;
-
   const f3 cam = mk(P.cx, P.cy, P.cz), light = mk(P.Lx, P.Ly, P.Lz);
-  f3 dir = primary_dir(P, (float)x / (float)P.W, (float)y / (float)P.H);
+  const f3 dir = primary_dir(P, (float)x / P.fW, (float)y / P.fH);
   float t;
-  int ind = closest_hit<ALLSPH>(geo, geo2, n, cam, dir, 0.0f, t);
+  int ind;
+  if (ALLSPH) {
+    const ConeF cone = wave_tile_cone(P);
+    ind = closest_hit_cone(geo, n, cone, cam, dir, 0.0f, t);
+  } else {
+    ind = closest_hit<ALLSPH>(geo, geo2, n, cam, dir, 0.0f, t);
+  }
+  count_work(P, active, y, 1u, active && ind != -1 ? 1u : 0u);
+  if (!active) return;
   float r, g, b;
   if (ind == -1) {
     r = P.bg.x; g = P.bg.y; b = P.bg.z;
@@ -148,25 +244,43 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
 // ---------------------------------------------------------------------------------------
 template <bool ALLSPH>
 __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
-  extern __shared__ float4 lds[];
-  stage_shapes(P, lds);
-  __syncthreads();
+  extern __shared__ float4 lds[];  // general scenes: LDS table; all-sphere: scalar path (phong_kernel)
+  if (!ALLSPH) {
+    stage_shapes(P, lds);
+    __syncthreads();
+  }
   const int n = P.nobj;
-  const float4 *geo = lds, *geo2 = lds + n, *col = lds + 2 * n, *aux = lds + 3 * n;
+  const float4* geo = ALLSPH ? P.shapes : lds;
+  const int stride = ALLSPH ? P.S : n;
+  const float4 *geo2 = geo + stride, *col = geo + 2 * stride, *aux = geo + 3 * stride;
   int x, y;
   tile_xy(x, y, P.trace_row0);
   const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
   const f3 light = mk(P.Lx, P.Ly, P.Lz);
   f3 pos = mk(P.cx, P.cy, P.cz);
-  f3 dir = primary_dir(P, (float)x / (float)P.W, (float)y / (float)P.H);
+  f3 dir = primary_dir(P, (float)x / P.fW, (float)y / P.fH);
   float arefl = 0.0f;          // array[2].w
   float rr = 0, rg = 0, rb = 0;  // result_color.rgb
   float c = 0.0f;
   unsigned nseg = 0, nshadow = 0;
+  float t0 = -1.0f;
+  int ind0 = -1;
+  if (ALLSPH) {  // the camera rays of the wave's 8x8 tile, cone-culled (every lane takes part)
+    const ConeF cone = wave_tile_cone(P);
+    ind0 = closest_hit_cone(geo, n, cone, pos, dir, 0.001f, t0);
+  }
   for (int seg = 0; active && seg < P.D; ++seg) {  // helper depth D, D-1, ..., 1
     // ---- hybrid_helper ----
     float t;
-    int ind = closest_hit<ALLSPH>(geo, geo2, n, pos, dir, 0.001f, t);
+    int ind;
+    if (ALLSPH && seg == 0) {  // camera rays: culled before the loop, with the whole wave
+      t = t0;
+      ind = ind0;
+    } else if (ALLSPH) {
+      ind = closest_hit_pf(geo, n, pos, dir, 0.001f, t);
+    } else {
+      ind = closest_hit<ALLSPH>(geo, geo2, n, pos, dir, 0.001f, t);
+    }
     ++nseg;
     nshadow += ind == -1 ? 0u : 1u;
     float ar, ag, ab;
@@ -348,69 +462,6 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4*
   d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
   P.dep[off] = d;
   store_color(P, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
-}
-
-// ---------------------------------------------------------------------------------------
-// Primary-ray cone culling (used by ao_batch_kernel).  Every primary ray starts at the camera
-// and passes through the pool's pixel rectangle (jitter < 0.0834 px), so one cone bounds
-// them.  A sphere whose line distance from every ray of the cone exceeds its radius by a
-// float-error margin has a computed discriminant < 0 for every lane (-1 in the reference,
-// never accepted) and is skipped.
-// ---------------------------------------------------------------------------------------
-constexpr int kPool = 256;
-constexpr int kSetupCost = 24;
-constexpr int kTailMaxObj = 128;  // split tail rounds stage the sphere table in LDS up to this size  // per-sample setup (hashes, directions, shading) in sphere-test units
-
-// Float form of the same cull (no trig): cone axis a, cos/sin of the half-angle; a sphere
-// with inflated radius r_eff (r_eff^2 = r^2 + 1e-5 (d^2 + r^2)) lies outside the forward and
-// the backward cone iff |cos phi| < cos(theta + alpha), sin alpha = r_eff / d.  Float error
-// (~1e-6) is covered by the 2e-5 slack on the cosine and the 1e-5 inflation.
-struct ConeF {
-  float ax, ay, az, ct, st;
-};
-
-// The cone only has to be conservative, not bit-exact: it is built with the raw
-// v_rcp/v_sqrt/v_rsq instructions (<= 1 ulp, ~1e-7 relative), far inside the 2e-5 cosine
-// slack and the 1e-5 radius inflation.
-__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
-__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
-__device__ __forceinline__ float fast_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
-
-__device__ inline ConeF pool_cone_f(const FrameParams& P, int xmin, int xmax, int ymin, int ymax) {
-  const float iw = fast_rcp(P.fW), ih = fast_rcp(P.fH);
-  const float hps[2] = {((float)xmin - 0.1f) * iw, ((float)xmax + 0.1f) * iw};
-  const float vps[2] = {((float)ymin - 0.1f) * ih, ((float)ymax + 0.1f) * ih};
-  f3 d[4];
-  f3 sum = mk(0.0f, 0.0f, 0.0f);
-  for (int k = 0; k < 4; ++k) {
-    float hp = hps[k & 1], vp = vps[k >> 1];
-    f3 v = mk(P.lx + hp * P.hx + vp * P.vx, P.ly + hp * P.hy + vp * P.vy, P.lz + hp * P.hz + vp * P.vz);
-    d[k] = fast_rsq(dot(v, v)) * v;
-    sum = sum + d[k];
-  }
-  const float il = fast_rsq(dot(sum, sum));
-  ConeF c;
-  c.ax = sum.x * il; c.ay = sum.y * il; c.az = sum.z * il;
-  float ct = 1.0f;
-  for (int k = 0; k < 4; ++k) ct = fminf(ct, c.ax * d[k].x + c.ay * d[k].y + c.az * d[k].z);
-  ct = fminf(fmaxf(ct - 2e-5f, -1.0f), 1.0f);  // widen the cone a little (direction rounding)
-  c.ct = ct;
-  c.st = fast_sqrt(fmaxf(0.0f, 1.0f - ct * ct));
-  return c;
-}
-
-__device__ inline bool cone_misses_f(const ConeF& c, float4 g, float cx, float cy, float cz) {
-  float Lx = g.x - cx, Ly = g.y - cy, Lz = g.z - cz;
-  float d2 = Lx * Lx + Ly * Ly + Lz * Lz, r2 = g.w * g.w;
-  float reff2 = r2 + 1e-5f * (d2 + r2);
-  if (!(d2 > reff2 * 1.01f + 1e-6f)) return false;  // camera inside / near the sphere: keep
-  float id = fast_rsq(d2);
-  float sa2 = reff2 * (id * id);
-  float sa = fast_sqrt(sa2), ca = fast_sqrt(fmaxf(0.0f, 1.0f - sa2));
-  float K = c.ct * ca - c.st * sa - 2e-5f;  // cos(theta + alpha), made smaller (conservative)
-  if (!(K > 0.0f)) return false;
-  float cphi = (c.ax * Lx + c.ay * Ly + c.az * Lz) * id;
-  return fabsf(cphi) < K;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1363,11 +1414,11 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
   dim3 grid((p.W + 15) / 16, (p.trace_rows + 15) / 16);
   switch (program) {
     case K_PHONG:
-      if (all_spheres) hipLaunchKernelGGL(phong_kernel<true>, grid, dim3(kBlock), lds, stream, p);
+      if (all_spheres) hipLaunchKernelGGL(phong_kernel<true>, grid, dim3(kBlock), 0, stream, p);
       else hipLaunchKernelGGL(phong_kernel<false>, grid, dim3(kBlock), lds, stream, p);
       break;
     case K_HYBRID:
-      if (all_spheres) hipLaunchKernelGGL(hybrid_kernel<true>, grid, dim3(kBlock), lds, stream, p);
+      if (all_spheres) hipLaunchKernelGGL(hybrid_kernel<true>, grid, dim3(kBlock), 0, stream, p);
       else hipLaunchKernelGGL(hybrid_kernel<false>, grid, dim3(kBlock), lds, stream, p);
       break;
     case K_POST:
