@@ -62,8 +62,8 @@ struct rt_ctx {
   int band0 = 0, band_rows = 0;  // strip + 1-row halo (post-process neighbours)
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  float4* d_shapes_buf[kAoStreams] = {};  // [4][S], one copy per AO stream
-  float4* d_rb_buf[kAoStreams] = {};      // [2*spp]
+  float4* d_shapes_buf[kAoStreams] = {};  // [4][S] table + [2*spp] rand_buffer, one copy per AO stream
+  float4* d_rb_buf[kAoStreams] = {};      // = d_shapes_buf[k] + 4*S (one allocation, one upload)
   float4* d_shapes = nullptr;  // the copy the next dispatch reads
   float4* d_rb = nullptr;
   std::vector<float4*> pix;    // F+pipe_depth buffers
@@ -168,7 +168,6 @@ void free_all(rt_ctx* c) {
   if (c->d_image_own) (void)hipFree(c->d_image_own);
   for (int k = 0; k < kAoStreams; ++k) {
     if (c->d_shapes_buf[k]) (void)hipFree(c->d_shapes_buf[k]);
-    if (c->d_rb_buf[k]) (void)hipFree(c->d_rb_buf[k]);
   }
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->d_row_counters) (void)hipFree(c->d_row_counters);
@@ -484,8 +483,9 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
   if (e == hipSuccess) e = hipMalloc(&x->d_image_own, (size_t)x->own_rows * c.width * sizeof(float4));
   if (e == hipSuccess) e = hipMemsetAsync(x->d_image_own, 0, (size_t)x->own_rows * c.width * sizeof(float4), x->stream);
   for (int k = 0; k < kAoStreams; ++k) {
-    if (e == hipSuccess) e = hipMalloc(&x->d_shapes_buf[k], (size_t)4 * std::max(1, c.num_shapes) * sizeof(float4));
-    if (e == hipSuccess) e = hipMalloc(&x->d_rb_buf[k], (size_t)2 * c.spp * sizeof(float4));
+    if (e == hipSuccess)
+      e = hipMalloc(&x->d_shapes_buf[k], ((size_t)4 * std::max(1, c.num_shapes) + (size_t)2 * c.spp) * sizeof(float4));
+    if (e == hipSuccess) x->d_rb_buf[k] = x->d_shapes_buf[k] + (size_t)4 * std::max(1, c.num_shapes);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(x->stream);
   if (e != hipSuccess) {
@@ -508,7 +508,7 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
   x->d_rb = x->d_rb_buf[0];
   x->out_stream = x->own_stream;
   x->header.assign(rt_header_bytes(c.num_shapes, c.spp) / 4, 0.0f);
-  x->table.assign((size_t)4 * std::max(1, c.num_shapes), make_float4(0, 0, 0, 0));
+  x->table.assign((size_t)4 * std::max(1, c.num_shapes) + (size_t)2 * c.spp, make_float4(0, 0, 0, 0));
   *out = x;
   return RT_OK;
 }
@@ -616,10 +616,9 @@ int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
     int sr = start_sequence(c);
     if (sr != RT_OK) return sr;
   }
-  int rc = staged_copy(c, c->d_shapes_buf[hc], c->table.data(), (size_t)4 * std::max(1, S) * sizeof(float4),
-                       ao_stream(c));
-  if (rc != RT_OK) return rc;
-  rc = staged_copy(c, c->d_rb_buf[hc], h + rt_off_rand(S) / 4, (size_t)2 * spp * sizeof(float4), ao_stream(c));
+  // table + rand_buffer in one upload (per-frame host cost matters for small strips/frames)
+  std::memcpy(c->table.data() + (size_t)4 * std::max(1, S), h + rt_off_rand(S) / 4, (size_t)2 * spp * sizeof(float4));
+  int rc = staged_copy(c, c->d_shapes_buf[hc], c->table.data(), c->table.size() * sizeof(float4), ao_stream(c));
   if (rc != RT_OK) return rc;
   c->d_shapes = c->d_shapes_buf[hc];
   c->d_rb = c->d_rb_buf[hc];
@@ -632,6 +631,7 @@ int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
 int rt_upload_rand_buffer(rt_ctx* c, const float* rb, size_t n_vec4) {
   if (!c || !rb || n_vec4 != (size_t)2 * c->cfg.spp) return RT_E_INVAL;
   std::memcpy(c->header.data() + rt_off_rand(c->cfg.num_shapes) / 4, rb, n_vec4 * 16);
+  std::memcpy(c->table.data() + (size_t)4 * std::max(1, c->cfg.num_shapes), rb, n_vec4 * 16);
   RT_HIP(c, hipSetDevice(c->device));
   const int hc = hdr_copy(c);
   int rc = staged_copy(c, c->d_rb_buf[hc], rb, n_vec4 * 16, ao_stream(c));
