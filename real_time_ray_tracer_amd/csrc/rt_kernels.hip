@@ -187,6 +187,76 @@ __device__ __forceinline__ ConeF wave_tile_cone(const FrameParams& P) {
   return pool_cone_f(P, x0, x0 + 7, y0, y0 + 7);
 }
 
+// shadow_ray (p_compute.glsl:145-166) for the whole wave at once, all-sphere scenes: every
+// shadow line passes (within ~3e-5) through the light, so the lines of the lanes that need
+// one lie in a cone with its apex at the light.  Spheres outside that cone (radius inflated
+// by 1e-4 plus cone_misses_f's margins) are missed by every line (-1, never an occluder); the
+// rest are tested as shadow_lit does.  "Some occluder exists" does not depend on the order.
+// Must be called by every lane of the wave (ballots and shuffles).
+constexpr int kShadowConeMinObj = 8;
+__device__ __forceinline__ bool shadow_lit_cone(const float4* __restrict__ geo, int n, f3 light, f3 pos, bool need) {
+  const f3 lv = light - pos;
+  const f3 l = normalize(lv);
+  const float len = sqrtf(dot(lv, lv));
+  const f3 np = pos + 0.01f * l;
+  const double dlen = (double)len;
+  if (__ballot(need) == 0) return true;
+  if (n <= kShadowConeMinObj) {  // small scenes: the cone costs more than it saves
+    bool lit = true;
+    for (int k = 0; k < n; ++k) {
+      if (need && lit) {
+        const double t = (double)sphere_eval(np, l, geo[k]);
+        if (t > (double)0.0001f) {
+          const double dx = t * (double)l.x, dy = t * (double)l.y, dz = t * (double)l.z;
+          if (sqrt(fma(dz, dz, fma(dy, dy, dx * dx))) < dlen) lit = false;
+        }
+      }
+    }
+    return lit;
+  }
+  // cone at the light over the directions -l of the lanes that need a shadow ray
+  float sx = need ? -l.x : 0.0f, sy = need ? -l.y : 0.0f, sz = need ? -l.z : 0.0f;
+  for (int o = 32; o > 0; o >>= 1) {
+    sx += __shfl_xor(sx, o);
+    sy += __shfl_xor(sy, o);
+    sz += __shfl_xor(sz, o);
+  }
+  const float il = __builtin_amdgcn_rsqf(sx * sx + sy * sy + sz * sz);
+  ConeF cone;
+  cone.ax = sx * il; cone.ay = sy * il; cone.az = sz * il;
+  float cd = need ? -(cone.ax * l.x + cone.ay * l.y + cone.az * l.z) : 1.0f;
+  for (int o = 32; o > 0; o >>= 1) cd = fminf(cd, __shfl_xor(cd, o));
+  cd = fminf(fmaxf(cd - 2e-5f, -1.0f), 1.0f);
+  cone.ct = cd;
+  cone.st = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - cd * cd));
+  const bool wide = !(cd > 0.05f);  // nearly a half-space: test everything
+  bool lit = true;
+  const int lane = threadIdx.x & 63;
+  for (int w = 0; w < n; w += 64) {
+    const int i = w + lane;
+    bool keep = i < n;
+    if (keep && !wide) {
+      const float4 g = geo[i];
+      keep = !cone_misses_f(cone, make_float4(g.x, g.y, g.z, g.w + 1e-4f), light.x, light.y, light.z);
+    }
+    unsigned long long m = __ballot(keep);
+    m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
+        (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
+    while (m) {
+      const int k = w + __builtin_ctzll(m);
+      m &= m - 1;
+      if (need && lit) {
+        const double t = (double)sphere_eval(np, l, geo[k]);
+        if (t > (double)0.0001f) {
+          const double dx = t * (double)l.x, dy = t * (double)l.y, dz = t * (double)l.z;
+          if (sqrt(fma(dz, dz, fma(dy, dy, dx * dx))) < dlen) lit = false;
+        }
+      }
+    }
+  }
+  return lit;
+}
+
 // ---------------------------------------------------------------------------------------
 // mode 3 — p_compute.glsl:168-245
 // ---------------------------------------------------------------------------------------
@@ -216,13 +286,16 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
     ind = closest_hit<ALLSPH>(geo, geo2, n, cam, dir, 0.0f, t);
   }
   count_work(P, active, y, 1u, active && ind != -1 ? 1u : 0u);
+  const bool need = active && ind != -1;
+  bool lit_w = true;
+  if (ALLSPH) lit_w = shadow_lit_cone(geo, n, light, cam + t * dir, need);  // every lane takes part
   if (!active) return;
   float r, g, b;
   if (ind == -1) {
     r = P.bg.x; g = P.bg.y; b = P.bg.z;
   } else {
     f3 curr = cam + t * dir;
-    bool lit = shadow_lit<ALLSPH>(geo, geo2, n, light, curr);
+    bool lit = ALLSPH ? lit_w : shadow_lit<ALLSPH>(geo, geo2, n, light, curr);
     int id = ALLSPH ? SHAPE_SPHERE : __float_as_int(geo2[ind].w);
     f3 nn = shape_normal(geo[ind], id, curr);
     float4 c = col[ind];
@@ -265,9 +338,11 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
   unsigned nseg = 0, nshadow = 0;
   float t0 = -1.0f;
   int ind0 = -1;
-  if (ALLSPH) {  // the camera rays of the wave's 8x8 tile, cone-culled (every lane takes part)
+  bool lit0 = true;
+  if (ALLSPH) {  // the camera rays of the wave's 8x8 tile and their shadow rays, cone-culled
     const ConeF cone = wave_tile_cone(P);
     ind0 = closest_hit_cone(geo, n, cone, pos, dir, 0.001f, t0);
+    lit0 = shadow_lit_cone(geo, n, light, pos + t0 * dir, active && ind0 != -1);  // every lane takes part
   }
   for (int seg = 0; active && seg < P.D; ++seg) {  // helper depth D, D-1, ..., 1
     // ---- hybrid_helper ----
@@ -291,7 +366,7 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
     } else {
       float4 att = col[ind];
       f3 curr = pos + t * dir;
-      bool lit = shadow_lit<ALLSPH>(geo, geo2, n, light, curr);
+      bool lit = (ALLSPH && seg == 0) ? lit0 : shadow_lit<ALLSPH>(geo, geo2, n, light, curr);
       int id = ALLSPH ? SHAPE_SPHERE : __float_as_int(geo2[ind].w);
       f3 nn = shape_normal(geo[ind], id, curr);
       if (lit) {
