@@ -15,6 +15,10 @@ timeout -k 10 400 python bench.py --config "$CFG" --steps "$STEPS" --warmup 8 > 
 cat "$OUT/bench.json"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
   python3 bench.py --config "$CFG" --steps 10 --warmup 8 --no-cpu-baseline > "$OUT/kt_bench.json" 2> "$OUT/kt.err"
+# the same bench sequential (--no-pipeline): every launch is a real kernel duration, so the
+# rocprof --stats averages compare directly with the bench line's kernel_ms
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_seq" -o run -- \
+  python3 bench.py --config "$CFG" --steps 10 --warmup 8 --no-cpu-baseline --no-pipeline > "$OUT/kt_seq_bench.json" 2> "$OUT/kt_seq.err"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
   python3 bench.py --config "$CFG" --steps 3 --warmup 8 --no-cpu-baseline > /dev/null 2> "$OUT/pmc_fetch.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
