@@ -79,6 +79,23 @@ __device__ __forceinline__ float sqrt_rn(float x) {
   return tiny ? s * 0x1p-16f : s;
 }
 
+// sqrt_rn without the tiny-input scaling, for the hit tail of sphere_candidate when the
+// acceptance threshold is >= 1e-6.  Equal to sqrt_rn for x >= 2^-96.  Below that it returns
+// some value in [0, 2^-47] (v_sqrt may flush or approximate there), and no caller can tell:
+// with s < 2^-47 and |b| >= 2^-22, s is below a quarter ulp of b, so fl(-b + s) and
+// fl(-b - s) are both -b whatever s is; with |b| < 2^-22 both roots are below 2.4e-7 in
+// magnitude and never pass the threshold.  Accepted t and index are therefore unchanged.
+__device__ __forceinline__ float sqrt_rn_tail(float x) {
+  float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __int_as_float(__float_as_int(s) - 1);
+  const float sp = __int_as_float(__float_as_int(s) + 1);
+  const float rm = fmaf(-sm, s, x);
+  const float rp = fmaf(-sp, s, x);
+  s = (rm <= 0.0f) ? sm : s;
+  s = (rp > 0.0f) ? sp : s;
+  return s;
+}
+
 // random(vec2), p_compute.glsl:65-75
 __device__ __forceinline__ float grandom(float sx, float sy) {
   float d = fmaf(sy, 78.233f, sx * 12.9898f);
@@ -177,7 +194,7 @@ __device__ __forceinline__ void sphere_candidate(f3 pos, f3 dir, float4 g, int i
     // -b, so the reference's (del == 0 ? -b : root choice) differs only in values <= 0, and
     // (t2 < 0 ? t1 : t2) differs from (t2 < 0 ? (t1 < 0 ? -1 : t1) : t2) only when t1 < 0:
     // none of these is ever accepted (thr > 0).  Accepted t and index are unchanged.
-    float s = sqrt_rn(del);
+    float s = thr >= 1e-6f ? sqrt_rn_tail(del) : sqrt_rn(del);  // thr is a literal at every call
     float t1 = -1.0f * b + s;
     float t2 = -1.0f * b - s;
     float res = (t2 < 0.0f) ? t1 : t2;

@@ -18,6 +18,7 @@ struct FrameParams {
   int nobj;                  // int(mode.z)
   int S;                     // stride of the compact shape table (capacity)
   int spp, D, F, frame;
+  int b1_min;                // AO: least live lanes of a prepared batch for its batched first bounce (set at launch)
   float inv_spp, fW, fH;     // 1.0f / spp, (float)W, (float)H: host-computed wave-uniform constants
   float hx, hy, hz;          // horizontal
   float vx, vy, vz;          // vertical

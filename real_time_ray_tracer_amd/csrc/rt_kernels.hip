@@ -67,6 +67,26 @@ __device__ __forceinline__ unsigned wave_max(unsigned v) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor(v, o));
   return v;
 }
+// Float wave reductions over all 64 lanes on the DPP path (quad perms, row mirrors, row
+// broadcasts), result read from lane 63 (wave-uniform).  The whole wave must be active.
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROWMASK, 0xf, false));
+}
+template <typename Op>
+__device__ __forceinline__ float wave_reduce_f(float v, Op op) {
+  v = op(v, dpp_f<0xB1>(v));        // quad_perm [1,0,3,2]
+  v = op(v, dpp_f<0x4E>(v));        // quad_perm [2,3,0,1]
+  v = op(v, dpp_f<0x141>(v));       // row_half_mirror: 8 lanes
+  v = op(v, dpp_f<0x140>(v));       // row_mirror: 16 lanes
+  v = op(v, dpp_f<0x142, 0xA>(v));  // row_bcast:15 into rows 1, 3
+  v = op(v, dpp_f<0x143, 0xC>(v));  // row_bcast:31 into rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_min_f(float v) { return wave_reduce_f(v, [](float a, float b) { return fminf(a, b); }); }
+__device__ __forceinline__ float wave_max_f(float v) { return wave_reduce_f(v, [](float a, float b) { return fmaxf(a, b); }); }
+__device__ __forceinline__ float wave_sum_f(float v) { return wave_reduce_f(v, [](float a, float b) { return a + b; }); }
+
 __device__ __forceinline__ void count_work(const FrameParams& P, bool active, int y, unsigned segs, unsigned shadows) {
   if (P.row_counters && active) atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)(segs + shadows));
   if (!P.counters) return;
@@ -154,6 +174,61 @@ __device__ inline bool cone_misses_f(const ConeF& c, float4 g, float cx, float c
   if (!(K > 0.0f)) return false;
   float cphi = (c.ax * Lx + c.ay * Ly + c.az * Lz) * id;
   return fabsf(cphi) < K;
+}
+
+// First-bounce cone of a prepared batch (ao_batch_kernel).  The live lanes' bounce rays start
+// at primary hit points of the batch's few pixels and go into a hemisphere about the hit
+// normal (or around the mirror direction), so their origins lie in a small ball (centre o,
+// radius rho) and their directions in a cone (axis a, half-angle theta).  A sphere is skipped
+// for the whole batch when, for every such ray, the reference's test provably rejects it:
+//  (1) every origin is clearly outside the sphere: |c - o| - rho - r > 1e-2 (|c - o| + rho);
+//  (2) the forward cone from o misses the sphere inflated to r_eff + rho, r_eff^2 = r^2 +
+//      1e-5 (Lmax^2 + r^2): beta > theta + alpha with sin alpha = (r_eff + rho) / |c - o|.
+// A ray from p (|p - o| <= rho) that met B(c, r_eff) would give the ray from o with the same
+// direction a point within rho of it, so by (2) every ray's forward half-line misses
+// B(c, r_eff).  If its closest approach to c lies ahead, the line passes at distance >= r_eff
+// and the exact discriminant is <= -1e-5 (Lmax^2 + r^2), > 10x the computed-discriminant
+// error (~7e-7 Lmax^2): the computed del is < 0 (-1, never accepted).  If it lies behind, both
+// real roots are negative and, by (1), the larger one is below -(|p - c| - r) <= -1e-2 Lmax,
+// > 10x the computed-root error (sqrt of the del error, ~8.4e-4 Lmax): the computed roots are
+// negative, never above the 1e-4 threshold.  NaN anywhere fails a comparison and keeps the
+// sphere.  Must be called by every lane of the wave.
+struct ConeB {
+  float ox, oy, oz, rho, ax, ay, az, ct, st;
+};
+
+__device__ __forceinline__ ConeB bounce_cone(bool live, f3 p, f3 d, unsigned long long lm) {
+  ConeB c;
+  const int first = __builtin_ctzll(lm);
+  c.ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.x), first));
+  c.oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.y), first));
+  c.oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.z), first));
+  const float ex = p.x - c.ox, ey = p.y - c.oy, ez = p.z - c.oz;
+  const float e2 = wave_max_f(live ? ex * ex + ey * ey + ez * ez : 0.0f);
+  const float sx = wave_sum_f(live ? d.x : 0.0f), sy = wave_sum_f(live ? d.y : 0.0f), sz = wave_sum_f(live ? d.z : 0.0f);
+  c.rho = fast_sqrt(e2) * 1.0001f + 1e-6f * (fabsf(c.ox) + fabsf(c.oy) + fabsf(c.oz));
+  const float s2 = sx * sx + sy * sy + sz * sz;
+  const float il = fast_rsq(s2);
+  c.ax = sx * il; c.ay = sy * il; c.az = sz * il;
+  float ct = wave_min_f(live ? c.ax * d.x + c.ay * d.y + c.az * d.z : 1.0f) - 2e-5f;
+  if (!(s2 > 1e-6f)) ct = -1.0f;  // directions cancel: no usable axis
+  ct = fminf(fmaxf(ct, -1.0f), 1.0f);
+  c.ct = ct;
+  c.st = fast_sqrt(fmaxf(0.0f, 1.0f - ct * ct));
+  return c;
+}
+
+__device__ __forceinline__ bool bounce_cone_misses(const ConeB& c, float4 g) {
+  const float vx = g.x - c.ox, vy = g.y - c.oy, vz = g.z - c.oz;
+  const float L = fast_sqrt(vx * vx + vy * vy + vz * vz);
+  const float r = fabsf(g.w), Lmax = L + c.rho;
+  if (!((L - c.rho - r) > 1e-2f * Lmax)) return false;  // (1)
+  const float R = fast_sqrt(r * r + 1e-5f * (Lmax * Lmax + r * r)) * 1.00001f + c.rho;
+  const float sa = R * fast_rcp(L), ca = fast_sqrt(fmaxf(0.0f, 1.0f - sa * sa));
+  if (!(c.st * ca + c.ct * sa > 1e-5f)) return false;  // theta + alpha >= pi: the cone covers the sphere
+  const float K = c.ct * ca - c.st * sa - 2e-5f;         // cos(theta + alpha), made smaller
+  const float cphi = (c.ax * vx + c.ay * vy + c.az * vz) * fast_rcp(L);
+  return cphi < K;  // (2)
 }
 
 // Closest hit of the camera rays of a pixel rectangle whose cone is `cone`: per 64-sphere
@@ -548,7 +623,7 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4*
 // handed to idle lanes by ds_bpermute whenever lanes run out of work.  Bounce rounds then
 // run with (nearly) all lanes live, and no per-sample setup runs at partial utilisation.
 // ---------------------------------------------------------------------------------------
-template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false>
+template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   extern __shared__ float4 lds[];
   const int spp = P.spp, W = P.W, D = P.D, nobj = P.nobj;
@@ -657,7 +732,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   int bitem = 0;
   f3 bpos = cam, bdir = cam, bhemi = cam;
   float br = 1.0f, bg = 1.0f, bb = 1.0f;
-  int next = 0, cursor = 0, nlive = 0;  // wave-uniform
+  int next = 0, cursor = 0, nlive = 0, bdepth = D - 1;  // wave-uniform
   unsigned nseg = 0;
   unsigned long long exec_tests = 0;
 
@@ -783,6 +858,39 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       if (LAZY && ind != -1 && !(aux[ind].x > 0.9f)) bhemi = hemisphere();
       live = shade(ind, t, bpos, bdir, bhemi, br, bg, bb, D, bitem, true);
     }
+    bdepth = D - 1;
+    if (B1) {
+      // The batch's live paths take their first bounce together, against the spheres their
+      // bounce cone does not exclude (bounce_cone), in ascending index order as closest_hit.
+      const unsigned long long lm1 = __ballot(live);
+      if (lm1 != 0 && __popcll(lm1) >= P.b1_min) {
+        lap(1);
+        const ConeB cb = bounce_cone(live, bpos, bdir, lm1);
+        float t = -1.0f;
+        int ind = -1;
+        for (int w = 0; w < nwords; ++w) {
+          const int i = (w << 6) + lane;
+          const bool keep = i < nobj && !bounce_cone_misses(cb, geo[i]);
+          unsigned long long m = __ballot(keep);
+          m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
+              (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
+          exec_tests += (unsigned long long)__popcll(m);
+          if (ABL == 3) tsec[6] += (unsigned long long)__popcll(m) << 24;  // sections: first-bounce survivors
+          if (live)
+            while (m) {
+              const int k = (w << 6) + __builtin_ctzll(m);
+              m &= m - 1;
+              sphere_candidate(bpos, bdir, geo[k], k, 0.0001f, t, ind);
+            }
+        }
+        if (live) {
+          ++nseg;
+          live = shade(ind, t, bpos, bdir, bhemi, br, bg, bb, D - 1, bitem, false);
+        }
+        bdepth = D - 2;
+        lap(4);  // sections: the batched first bounce (shares slot 4 with combine + stores)
+      }
+    }
     unsigned long long lm = __ballot(live);
     if (live) perm[__builtin_amdgcn_mbcnt_hi((unsigned)(lm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)lm, 0u))] = lane;
     nlive = __popcll(lm);
@@ -819,7 +927,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         hemi = mk(hx, hy, hz);
         rr = cr; rg = cg; rb = cb;
         item = ci;
-        depth = D - 1;
+        depth = bdepth;
         has = true;
       }
       cursor += take;
@@ -1448,15 +1556,22 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
     // lane-per-sample kernel (the general one, used for scenes with planes).
     const char* ev = getenv("RTRT_AO_VARIANT");
     const int variant = ev ? atoi(ev) : 7;
-    if (all_spheres && (variant == 7 || variant == 17 || variant == 11 || (variant >= 91 && variant <= 93))) {
+    const char* eb = getenv("RTRT_B1_MIN");
+    FrameParams q = p;
+    q.b1_min = eb ? atoi(eb) : 1;
+    if (all_spheres && (variant == 7 || variant == 27 || variant == 17 || variant == 11 || (variant >= 91 && variant <= 93))) {
       const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
       const long long pools = (npix + TP - 1) / TP;
       const size_t psh = (size_t)TP * sizeof(float4) + (size_t)3 * TP * p.spp * sizeof(float) + (size_t)TP * sizeof(int) +
                          (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8 +
                          16 + (size_t)2 * p.spp * sizeof(float4) +
-                         (variant == 7 && p.nobj <= kTailMaxObj ? (size_t)p.nobj * sizeof(float4) : 0);
+                         ((variant == 7 || variant == 27 || variant == 93) && p.nobj <= kTailMaxObj ? (size_t)p.nobj * sizeof(float4) : 0);
       const dim3 g((unsigned)pools), b(64);
       if (variant == 7 && p.nobj <= kTailMaxObj)  // split tail rounds (the sphere table fits in LDS)
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true>), g, b, psh, stream, q, p.shapes);
+      else if (variant == 7)
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true>), g, b, psh, stream, q, p.shapes);
+      else if (variant == 27 && p.nobj <= kTailMaxObj)  // 7 without the batched first bounce (A/B)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true>), g, b, psh, stream, p, p.shapes);
       else if (variant == 11)
         hipLaunchKernelGGL((ao_batch_kernel<7, false>), g, b, psh, stream, p, p.shapes);
@@ -1464,8 +1579,10 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 1>), g, b, psh, stream, p, p.shapes);
       else if (variant == 92)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2>), g, b, psh, stream, p, p.shapes);
+      else if (variant == 93 && p.nobj <= kTailMaxObj)  // section clocks of variant 7
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true>), g, b, psh, stream, q, p.shapes);
       else if (variant == 93)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3>), g, b, psh, stream, p, p.shapes);
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, false, true>), g, b, psh, stream, q, p.shapes);
       else  // 7 with a large scene, or 17: without the split tail rounds (A/B)
         hipLaunchKernelGGL(ao_batch_kernel<7>, g, b, psh, stream, p, p.shapes);
     } else if (all_spheres && (variant == 20 || variant == 25)) {

@@ -16,7 +16,7 @@ from bench import CONFIG_INDEX, CONFIGS  # noqa: E402
 from real_time_ray_tracer_amd import Header, Renderer, aspect_for  # noqa: E402
 
 NAMES = ["cull setup", "prepare (primary + first shade)", "hand-out / regeneration", "bounce test + shade",
-         "combine + stores"]
+         "first bounce (batched) + combine + stores"]
 
 
 def main():
@@ -43,6 +43,8 @@ def main():
     for n, v in zip(NAMES, vals):
         print(f"{n:34s} {v / 1e9:9.3f} Gclk  {100 * v / tot:5.1f}%")
     rounds, sum_ncull, prepares = c["post_pixels"], c["history_read"], c["history_accepted"]
+    b1_surv, sum_ncull = sum_ncull >> 24, sum_ncull & ((1 << 24) - 1)
+    print(f"batched first bounce: {b1_surv / max(prepares, 1):.2f} spheres tested per prepared batch (of {S})")
     print(f"bounce rounds {rounds}  prepares {prepares}  mean culled primary set {sum_ncull / max(prepares, 1):.2f}")
     print(f"bounce sphere-iterations per frame {rounds * S / 1e6:.1f} M; per 64-sample prepare batch "
           f"{rounds / max(prepares, 1):.2f} rounds")
