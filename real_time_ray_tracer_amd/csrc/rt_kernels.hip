@@ -757,44 +757,42 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   };
 
   // hit shading shared by primary and bounce segments; returns true when the path goes on
+  // (written with one exit: the attenuation product, the kind store and finish() each appear
+  // once, and the diffuse and mirror directions share their final normalize, so lanes that
+  // take different cases do not run duplicated code)
   auto shade = [&](int ind, float t, f3& ps, f3& dr, f3 hm, float& r, float& g, float& b, int dpt, int it,
                    bool first) -> bool {
     const int lp = div_spp(it), aa = it - lp * spp;
+    float4 att = P.bg;  // miss: background
+    int kind = PRIM_MISS;
+    bool go = false;
     if (ind != -1) {
-      float4 att = col[ind];
-      float4 ax = aux[ind];
-      if (ax.x > 0.9f) {
-        r = r * att.x; g = g * att.y; b = b * att.z;
-        if (aa == 0 && first) pkind[lp] = PRIM_EMISSIVE;
-        finish(it, r, g, b, (float)(D - dpt), D - dpt + 1);
-        return false;
-      }
-      f3 curr = cam + t * dr;  // sic: camera origin (ao_compute.glsl:210)
-      f3 nn = normalize(curr - xyz(geo[ind]));
-      if (aa == 0 && first) {
-        pkind[lp] = PRIM_HIT;
-        prec[lp] = make_float4(nn.x, nn.y, nn.z, t);
-      }
-      r = r * att.x; g = g * att.y; b = b * att.z;
-      ps = curr;
-      float reflect = ax.y;
-      if (reflect > 0.999f) {
-        dr = normalize(hm + nn);
+      att = col[ind];
+      if (aux[ind].x > 0.9f) {
+        kind = PRIM_EMISSIVE;
       } else {
-        float dn = dot(dr, nn);
-        f3 R = normalize(mk(dr.x - 2.0f * (dn * nn.x), dr.y - 2.0f * (dn * nn.y), dr.z - 2.0f * (dn * nn.z)));
-        dr = normalize(R + reflect * hm);
+        kind = PRIM_HIT;
+        f3 curr = cam + t * dr;  // sic: camera origin (ao_compute.glsl:210)
+        f3 nn = normalize(curr - xyz(geo[ind]));
+        if (aa == 0 && first) prec[lp] = make_float4(nn.x, nn.y, nn.z, t);
+        ps = curr;
+        const float reflect = aux[ind].y;
+        f3 X;
+        if (reflect > 0.999f) {
+          X = hm + nn;
+        } else {
+          float dn = dot(dr, nn);
+          f3 R = normalize(mk(dr.x - 2.0f * (dn * nn.x), dr.y - 2.0f * (dn * nn.y), dr.z - 2.0f * (dn * nn.z)));
+          X = R + reflect * hm;
+        }
+        dr = normalize(X);
+        go = dpt - 1 != 0;  // RECURSION_DEPTH non-emissive hits end without a stop write
       }
-      if (dpt - 1 == 0) {  // RECURSION_DEPTH non-emissive hits: no stop write
-        finish(it, r, g, b, -1.0f, D);
-        return false;
-      }
-      return true;
     }
-    if (aa == 0 && first) pkind[lp] = PRIM_MISS;
-    r = r * P.bg.x; g = g * P.bg.y; b = b * P.bg.z;
-    finish(it, r, g, b, (float)(D - dpt), D - dpt + 1);
-    return false;
+    r = r * att.x; g = g * att.y; b = b * att.z;
+    if (aa == 0 && first) pkind[lp] = kind;
+    if (!go) finish(it, r, g, b, kind == PRIM_HIT ? -1.0f : (float)(D - dpt), kind == PRIM_HIT ? D : D - dpt + 1);
+    return go;
   };
 
   // Prepare the next 64 samples with the whole wave.
