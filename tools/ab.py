@@ -5,6 +5,10 @@ the shim at launch) and records the per-launch HIP-event time of the trace kerne
 must be bit-identical across variants.
 
     python tools/ab.py --config d --variants 0,1,2 --rounds 3 --frames 4
+    python tools/ab.py --config d --libs build/old/librtrt.so,real_time_ray_tracer_amd/librtrt.so
+
+With --libs the variants are two (or more) builds of the library, each loaded as its own copy
+in the same process, so builds are compared on the same GPU clock state (and bit for bit).
 """
 import argparse
 import json
@@ -28,11 +32,25 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--frames", type=int, default=4)
     ap.add_argument("--env", default="RTRT_AO_VARIANT")
+    ap.add_argument("--libs", default="", help="comma-separated librtrt.so builds to compare instead of variants")
     ap.add_argument("--prog", type=int, default=0, help="program to time (default: the trace pass)")
     ap.add_argument("--time-from", type=int, default=1, help="first frame timed (history fills over 8 frames)")
     args = ap.parse_args()
     W, H, S, spp, mode, desc = CONFIGS[args.config]
     variants = [v for v in args.variants.split(",")]
+    libs = {}
+    if args.libs:
+        import ctypes as C
+        from real_time_ray_tracer_amd import _lib
+        _lib.load()  # torch first, then the default build (the Header helpers use it)
+        variants = args.libs.split(",")
+        for path in variants:
+            lib = C.CDLL(str(Path(path).resolve()), mode=C.RTLD_LOCAL)
+            for name, (res, argt) in _lib.SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = argt
+            libs[path] = lib
     h = Header.synthetic(S, spp, 1234 + CONFIG_INDEX[args.config], aspect_for(W, H))
     prog = args.prog or {1: 1, 2: 3, 3: 4, 4: 5}[mode]
     times = {v: [] for v in variants}
@@ -40,7 +58,11 @@ def main():
     counts = None
     for rnd in range(args.rounds):
         for v in variants:
-            os.environ[args.env] = v
+            if libs:
+                from real_time_ray_tracer_amd import _lib
+                _lib._LIB = libs[v]
+            else:
+                os.environ[args.env] = v
             r = Renderer(W, H, S, spp)
             if rnd == 0 and v == variants[0]:
                 r.enable_counters(True)
