@@ -733,6 +733,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   f3 bpos = cam, bdir = cam, bhemi = cam;
   float br = 1.0f, bg = 1.0f, bb = 1.0f;
   int next = 0, cursor = 0, nlive = 0, bdepth = D - 1;  // wave-uniform
+  int b1cost = nobj;  // spheres the latest batched first bounce tested (row cost profile)
   unsigned nseg = 0;
   unsigned long long exec_tests = 0;
 
@@ -752,7 +753,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       int x, y;
       pool_xy(div_spp(it), x, y);
       atomicAdd(&P.row_counters[y - P.band_row0],
-                (unsigned long long)(kSetupCost + ncull + (segs - 1) * nobj));
+                (unsigned long long)(kSetupCost + ncull + (segs >= 2 ? b1cost + (segs - 2) * nobj : 0)));
     }
   };
 
@@ -857,6 +858,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       live = shade(ind, t, bpos, bdir, bhemi, br, bg, bb, D, bitem, true);
     }
     bdepth = D - 1;
+    b1cost = nobj;
     if (B1) {
       // The batch's live paths take their first bounce together, against the spheres their
       // bounce cone does not exclude (bounce_cone), in ascending index order as closest_hit.
@@ -866,6 +868,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         const ConeB cb = bounce_cone(live, bpos, bdir, lm1);
         float t = -1.0f;
         int ind = -1;
+        b1cost = 0;
         for (int w = 0; w < nwords; ++w) {
           const int i = (w << 6) + lane;
           const bool keep = i < nobj && !bounce_cone_misses(cb, geo[i]);
@@ -873,6 +876,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
               (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
           exec_tests += (unsigned long long)__popcll(m);
+          b1cost += __popcll(m);
           if (ABL == 3) tsec[6] += (unsigned long long)__popcll(m) << 24;  // sections: first-bounce survivors
           if (live)
             while (m) {

@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--equal", action="store_true")
     ap.add_argument("--kernels", action="store_true", help="sum of kernel times (sequential) instead of frame wall time")
     ap.add_argument("--only", type=int, default=-1, help="time only this strip (e.g. under rocprofv3)")
+    ap.add_argument("--calibrate", action="store_true",
+                    help="bench.py's calibration: time the plan's strips (kernel sums), rescale the profile, "
+                         "re-balance; best of three measured plans")
     a = ap.parse_args()
     W, H, S, spp, mode, _ = CONFIGS[a.config]
     h = Header.synthetic(S, spp, 1234 + CONFIG_INDEX[a.config], aspect_for(W, H))
@@ -72,6 +75,17 @@ def main():
         cost = r.read_row_counters().astype(np.float64)
         r.close()
         b = balanced_bounds(cost, a.n)
+        if a.calibrate:
+            from real_time_ray_tracer_amd.dist import calibrate_row_cost
+            measured = []
+            for it in range(3):
+                t = [frame_ms(W, H, S, spp, mode, h, (b[i], b[i + 1]), 3, warm=3, kernels=True) for i in range(a.n)]
+                measured.append((max(t), list(b)))
+                print(f"calibration plan {it}: {b} kernel-sum ms {[round(x, 3) for x in t]}")
+                if it < 2:
+                    cost = calibrate_row_cost(b, cost, t)
+                    b = balanced_bounds(cost, a.n)
+            b = min(measured, key=lambda m: m[0])[1]
     strips, host = [], []
     for i in range(a.n):
         if a.only >= 0 and i != a.only:
