@@ -46,7 +46,8 @@ __device__ __forceinline__ float gclamp(float x, float lo, float hi) { return gm
 // ~5e5 at 8K).  GLSL leaves sin's precision for large arguments unspecified; what matters
 // for random() is that host and device compute the same value.
 __device__ __forceinline__ float det_sin(float x) {
-  if (!(fabsf(x) <= 3.40282347e38f)) return x - x;
+  // (no explicit inf/NaN test: k = rint(+-inf) = +-inf makes r = NaN, and NaN stays NaN, so
+  // both return NaN as the oracle's x - x does)
   float k = rintf(x * 0.636619772f);
   float r = fmaf(-k, 1.57079637f, x);
   r = fmaf(-k, -4.37113883e-08f, r);

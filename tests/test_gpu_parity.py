@@ -181,6 +181,8 @@ def test_math_primitives_bitwise():
                         [0.0, -0.0, 1e-30, 3.14159265, 1.5707964, 1e6, 3e7]]).astype(np.float32)
     ref = oracle.det_sin(x)
     assert_bitwise(r.selftest_math(_lib.RT_MATH_SIN, x, x.size), ref, "det_sin")
+    bad = np.array([np.inf, -np.inf, np.nan], np.float32)
+    assert np.isnan(r.selftest_math(_lib.RT_MATH_SIN, bad, bad.size)).all() and np.isnan(oracle.det_sin(bad)).all()
     xy = rng.uniform(0, 8000, (20000, 2)).astype(np.float32)
     assert_bitwise(r.selftest_math(_lib.RT_MATH_RANDOM, xy, len(xy)), oracle.random2(xy), "random")
     v = np.concatenate([rng.uniform(0, 1e6, 100000), 10.0 ** rng.uniform(-45, 38.5, 100000),
