@@ -256,6 +256,62 @@ __device__ __forceinline__ int closest_hit_pf(const float4* __restrict__ geo, in
   return ind;
 }
 
+// closest_hit_pf over the n <= 64 spheres geo[0..n) (indices base + i) whose bit is set in the
+// wave-uniform mask m: the table is still streamed 4 spheres per scalar load, prefetched one
+// group ahead, and a sphere whose bit is clear is skipped by a scalar branch.  Ascending order
+// with the strict '<' of sphere_candidate, so the result equals closest_hit's on the set bits.
+__device__ __forceinline__ void closest_hit_pf_masked(const float4* __restrict__ geo, int n, int base,
+                                                      unsigned long long m, f3 pos, f3 dir, float thr, float& t,
+                                                      int& ind) {
+  int i = 0;
+  if (n >= 4) {
+    float4 g0 = geo[0], g1 = geo[1], g2 = geo[2], g3 = geo[3];
+    for (; i + 8 <= n; i += 4) {
+      float4 n0 = geo[i + 4], n1 = geo[i + 5], n2 = geo[i + 6], n3 = geo[i + 7];
+      const unsigned nib = (unsigned)(m >> i) & 0xfu;
+      if (nib) {
+        if (nib & 1u) sphere_candidate(pos, dir, g0, base + i, thr, t, ind);
+        if (nib & 2u) sphere_candidate(pos, dir, g1, base + i + 1, thr, t, ind);
+        if (nib & 4u) sphere_candidate(pos, dir, g2, base + i + 2, thr, t, ind);
+        if (nib & 8u) sphere_candidate(pos, dir, g3, base + i + 3, thr, t, ind);
+      }
+      g0 = n0; g1 = n1; g2 = n2; g3 = n3;
+    }
+    const unsigned nib = (unsigned)(m >> i) & 0xfu;
+    if (nib & 1u) sphere_candidate(pos, dir, g0, base + i, thr, t, ind);
+    if (nib & 2u) sphere_candidate(pos, dir, g1, base + i + 1, thr, t, ind);
+    if (nib & 4u) sphere_candidate(pos, dir, g2, base + i + 2, thr, t, ind);
+    if (nib & 8u) sphere_candidate(pos, dir, g3, base + i + 3, thr, t, ind);
+    i += 4;
+  }
+  for (; i < n; ++i)
+    if ((m >> i) & 1ull) sphere_candidate(pos, dir, geo[i], base + i, thr, t, ind);
+}
+
+// closest_hit_pf with groups of 2 spheres (one s_load_dwordx8 each): half the scalar registers
+// of the 4-sphere pipeline.  Same visiting order and acceptance (bit-identical).
+__device__ __forceinline__ int closest_hit_pf2(const float4* __restrict__ geo, int nobj, f3 pos, f3 dir, float thr,
+                                               float& t_out) {
+  float t = -1.0f;
+  int ind = -1;
+  int i = 0;
+  if (nobj >= 2) {
+    float4 g0 = geo[0], g1 = geo[1];
+    for (; i + 4 <= nobj; i += 2) {
+      float4 n0 = geo[i + 2], n1 = geo[i + 3];
+      sphere_candidate(pos, dir, g0, i, thr, t, ind);
+      sphere_candidate(pos, dir, g1, i + 1, thr, t, ind);
+      g0 = n0; g1 = n1;
+    }
+    sphere_candidate(pos, dir, g0, i, thr, t, ind);
+    sphere_candidate(pos, dir, g1, i + 1, thr, t, ind);
+    i += 2;
+  }
+  for (; i < nobj; ++i) sphere_candidate(pos, dir, geo[i], i, thr, t, ind);
+  t_out = t;
+  return ind;
+}
+
 // shadow_ray, p_compute.glsl:145-166: any occluder with double t > 0.0001 closer than the light
 template <bool ALLSPH>
 __device__ __forceinline__ bool shadow_lit(const float4* __restrict__ geo, const float4* __restrict__ geo2,

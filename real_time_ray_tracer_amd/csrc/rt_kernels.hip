@@ -981,7 +981,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     exec_tests += (unsigned long long)nobj;
     if (has) {
       float t;
-      int ind = closest_hit_pf(geo, nobj, pos, dir, 0.0001f, t);
+      int ind = closest_hit_pf2(geo, nobj, pos, dir, 0.0001f, t);
       if (ABL == 1) {  // timing ablation: the bounce tests twice
         float z, t2;
         asm volatile("v_mov_b32 %0, 0" : "=v"(z));
