@@ -623,25 +623,47 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4*
 // handed to idle lanes by ds_bpermute whenever lanes run out of work.  Bounce rounds then
 // run with (nearly) all lanes live, and no per-sample setup runs at partial utilisation.
 // ---------------------------------------------------------------------------------------
-template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false>
+// LDS layout of ao_batch_kernel, in bytes.  Every offset is a compile-time constant when spp
+// is (SPPC), so the kernel then holds no LDS addresses in scalar registers.
+struct BatchLds {
+  int prec, sres, pstop, pkind, perm, cmask, rls, geol, total;
+};
+__host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
+  const int TP = pool / spp > 0 ? pool / spp : 1, NS = TP * spp;
+  BatchLds L{};
+  L.prec = 0;                                   // [TP] float4: first-segment (normal, t) of sample 0
+  L.sres = 16 * TP;                             // [3][NS] float: per-sample r, g, b (channel-major)
+  L.pstop = L.sres + 12 * NS;                   // [TP] int: max (aa << 16 | stop) of the stop writes
+  L.pkind = L.pstop + 4 * TP;                   // [TP] int
+  L.perm = L.pkind + 4 * ((TP + 1) & ~1);       // [64] int: live rank -> lane of the prepared batch
+  L.cmask = (L.perm + 256 + 7) & ~7;            // [32] u64: primary cull mask (nobj <= 2048)
+  L.rls = (L.cmask + 8 * 32 + 15) & ~15;        // [2 spp] float4: rand_buffer
+  L.geol = L.rls + 32 * spp;                    // [ntail] float4: sphere table (split tail rounds)
+  L.total = L.geol + 16 * ntail;
+  return L;
+}
+
+template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
+          int SPPC = 0>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   extern __shared__ float4 lds[];
-  const int spp = P.spp, W = P.W, D = P.D, nobj = P.nobj;
+  const int spp = SPPC ? SPPC : P.spp, W = P.W, D = P.D, nobj = P.nobj;
   const int TP = POOL / spp > 0 ? POOL / spp : 1;
   const int lane = threadIdx.x;
   const int NS = TP * spp;
-  float4* prec = lds;                      // [TP] first-segment (normal, t) of sample 0
-  float* sres = (float*)(prec + TP);       // [3][NS] per-sample r, g, b (channel-major)
-  int* pstop = (int*)(sres + 3 * NS);      // [TP] max (aa << 16 | stop value) of the samples with a stop write
-  int* pkind = pstop + TP;                 // [TP]
-  int* perm = pkind + ((TP + 1) & ~1);     // [64] live-rank -> lane of the prepared batch
-  unsigned long long* cmask = (unsigned long long*)(perm + 64);  // [ceil(nobj/64)]
-  // [2*spp] rand_buffer staged in LDS (16-byte aligned after cmask)
-  float4* rls = (float4*)(((uintptr_t)(cmask + ((nobj + 63) >> 6)) + 15) & ~(uintptr_t)15);
+  const BatchLds LO = batch_lds(spp, POOL, 0);
+  char* lbase = (char*)lds;
+  float4* prec = (float4*)(lbase + LO.prec);
+  float* sres = (float*)(lbase + LO.sres);
+  int* pstop = (int*)(lbase + LO.pstop);
+  int* pkind = (int*)(lbase + LO.pkind);
+  int* perm = (int*)(lbase + LO.perm);
+  unsigned long long* cmask = (unsigned long long*)(lbase + LO.cmask);
+  float4* rls = (float4*)(lbase + LO.rls);
   for (int k = lane; k < 2 * spp; k += 64) rls[k] = P.rb[k];
   for (int k = lane; k < TP; k += 64) pstop[k] = -1;
   // TAIL: the sphere table in LDS (per-lane sphere indices in the split tail rounds)
-  float4* geol = rls + 2 * spp;  // [nobj] when TAIL && nobj <= kTailMaxObj
+  float4* geol = (float4*)(lbase + LO.geol);  // [nobj] when TAIL && nobj <= kTailMaxObj
   const bool tail_ok = TAIL && nobj <= kTailMaxObj;
   if (tail_ok)
     for (int k = lane; k < nobj; k += 64) geol[k] = geo[k];
@@ -739,7 +761,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
 
   const float inv_spp = P.inv_spp;
   // it / spp for pool items (< 2^16): exact via the float reciprocal (error << 0.5/spp)
-  auto div_spp = [&](int it) { return (int)(((float)it + 0.5f) * inv_spp); };
+  auto div_spp = [&](int it) { return SPPC ? (int)((unsigned)it / (unsigned)SPPC) : (int)(((float)it + 0.5f) * inv_spp); };
   // row cost profile (strip balancing), in sphere-test units: setup + culled primary + bounces
   auto finish = [&](int it, float r, float g, float b, float stopv, int segs) {
     sres[it] = r;
@@ -1014,6 +1036,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     pool_xy(lp, x, y);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
     const float* ps = sres + lp * spp;
+#pragma unroll 1
     for (int k = 0; k < spp; ++k) {
       sr = sr + ps[k]; sg = sg + ps[NS + k]; sb = sb + ps[2 * NS + k];
     }
@@ -1564,12 +1587,26 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
     if (all_spheres && (variant == 7 || variant == 27 || variant == 17 || variant == 11 || (variant >= 91 && variant <= 93))) {
       const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
       const long long pools = (npix + TP - 1) / TP;
-      const size_t psh = (size_t)TP * sizeof(float4) + (size_t)3 * TP * p.spp * sizeof(float) + (size_t)TP * sizeof(int) +
-                         (size_t)((TP + 1) & ~1) * sizeof(int) + 64 * sizeof(int) + (size_t)((p.nobj + 63) / 64 + 2) * 8 +
-                         16 + (size_t)2 * p.spp * sizeof(float4) +
-                         ((variant == 7 || variant == 27 || variant == 93) && p.nobj <= kTailMaxObj ? (size_t)p.nobj * sizeof(float4) : 0);
+      const size_t psh = (size_t)batch_lds(p.spp, kPool,
+                                           (variant == 7 || variant == 27 || variant == 93) && p.nobj <= kTailMaxObj
+                                               ? p.nobj : 0).total;
       const dim3 g((unsigned)pools), b(64);
-      if (variant == 7 && p.nobj <= kTailMaxObj)  // split tail rounds (the sphere table fits in LDS)
+      // spp 4, 16 and 64 (the reference's own scene, configs c/d, config e) have their own
+      // instantiations: constant LDS offsets and it / spp, fewer scalar registers (-5%)
+      const bool tl = p.nobj <= kTailMaxObj;
+      if (variant == 7 && p.spp == 16 && tl)
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 16>), g, b, psh, stream, q, p.shapes);
+      else if (variant == 7 && p.spp == 16)
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, 16>), g, b, psh, stream, q, p.shapes);
+      else if (variant == 7 && p.spp == 64 && tl)
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 64>), g, b, psh, stream, q, p.shapes);
+      else if (variant == 7 && p.spp == 64)
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, 64>), g, b, psh, stream, q, p.shapes);
+      else if (variant == 7 && p.spp == 4 && tl)
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 4>), g, b, psh, stream, q, p.shapes);
+      else if (variant == 7 && p.spp == 4)
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, 4>), g, b, psh, stream, q, p.shapes);
+      else if (variant == 7 && tl)  // split tail rounds (the sphere table fits in LDS)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true>), g, b, psh, stream, q, p.shapes);
       else if (variant == 7)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true>), g, b, psh, stream, q, p.shapes);
@@ -1581,7 +1618,9 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 1>), g, b, psh, stream, p, p.shapes);
       else if (variant == 92)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2>), g, b, psh, stream, p, p.shapes);
-      else if (variant == 93 && p.nobj <= kTailMaxObj)  // section clocks of variant 7
+      else if (variant == 93 && p.nobj <= kTailMaxObj && p.spp == 16)  // section clocks of variant 7
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true, 16>), g, b, psh, stream, q, p.shapes);
+      else if (variant == 93 && p.nobj <= kTailMaxObj)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true>), g, b, psh, stream, q, p.shapes);
       else if (variant == 93)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, false, true>), g, b, psh, stream, q, p.shapes);
