@@ -10,7 +10,7 @@ OBJDIR   := build/obj
 
 # -ffp-contract=off + correctly-rounded f32 '/' and sqrt: the float semantics shared with the
 # oracle (oracle/rt_oracle.h).  No fast-math anywhere.
-HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off \
+HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off $(HIPFLAGS_EXTRA) \
             -fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -Wall -Wno-unused-function -Iinclude
 CFLAGS_ORACLE := -O3 -march=x86-64-v3 -ffp-contract=off -fopenmp -fPIC -std=c99 -Wall
 

@@ -1545,6 +1545,19 @@ __global__ void selftest_kernel(int fn, const float* __restrict__ in, float* __r
       out[i] = (float)bad;
       break;
     }
+    case 7: {  // exhaustive inv_len_rn == 1/sqrtf over [0, 0x7f800000]; rcp_rn_normal == 1/x on [2^-126, 2^126]
+      const unsigned per = (unsigned)in[0];
+      unsigned bad = 0;
+      for (unsigned k = 0; k < per; ++k) {
+        unsigned long long u = (unsigned long long)i * per + k;
+        if (u > 0x7f800000ull) break;
+        float x = __uint_as_float((unsigned)u);
+        bad += __float_as_uint(inv_len_rn(x)) != __float_as_uint(1.0f / sqrtf(x));
+        if (u >= 0x00800000ull && u <= 0x7e800000ull) bad += __float_as_uint(rcp_rn_normal(x)) != __float_as_uint(1.0f / x);
+      }
+      out[i] = (float)bad;
+      break;
+    }
     case 3: out[i] = in[2 * i] / in[2 * i + 1]; break;
     case 4: {
       f3 v = normalize(mk(in[3 * i], in[3 * i + 1], in[3 * i + 2]));

@@ -204,6 +204,18 @@ def test_sqrt_rn_exhaustive():
     assert float(bad.sum()) == 0.0, f"{int(bad.sum())} mismatching inputs"
 
 
+def test_rcp_rn_exhaustive():
+    """normalize's 1/sqrt (sqrt_rn_tail + v_rcp_f32 + one Newton step, with the compiler's
+    sequence for out-of-range inputs) equals 1.0f/sqrtf on every non-negative float, and the
+    reciprocal step equals 1.0f/x on every normal x in [2^-126, 2^126], on the device."""
+    r = Renderer(8, 8, 1, 1)
+    per, n = 2048, 1 << 20
+    bad = r.selftest_math(_lib.RT_MATH_RCP_SWEEP, np.array([per], np.float32), n)
+    r.close()
+    assert n * per > 0x7f800000
+    assert float(bad.sum()) == 0.0, f"{int(bad.sum())} mismatching inputs"
+
+
 def test_errors_are_reported():
     r = Renderer(16, 16, 4, 4)
     with pytest.raises(_lib.RtError):
