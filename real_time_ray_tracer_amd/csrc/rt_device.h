@@ -42,6 +42,17 @@ __device__ __forceinline__ float inv_len_rn(float d) {
   if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) == 0, 1)) return rcp_rn_normal(sqrt_rn_tail(d));
   return 1.0f / sqrtf(d);
 }
+// a / b for a divisor b known ahead with y = 1.0f / b (correctly rounded): Markstein's
+// refinement q = a*y, r = fma(-b, q, a) (exact), q' = fma(r, y, q).  By Markstein's theorem
+// q' is the correctly rounded a / b whenever there is no underflow or overflow (a / b, y and
+// b normal); the device sweep tools/micro/div_sweep.hip finds no mismatch for a in
+// [2^-100, 2^100) with b = 6 and every configured width and height (mismatches appear only
+// where a / b is subnormal).  Callers pass a = 0, NaN, or |a| in [2^-40, 2^14].  3
+// instructions instead of the 11 of the IEEE division sequence.
+__device__ __forceinline__ float div_rn_by(float a, float b, float y) {
+  const float q = a * y;
+  return fmaf(fmaf(-b, q, a), y, q);
+}
 // GLSL normalize(): v * (1 / length(v)) with IEEE sqrt and division (GPU GLSL compilers
 // lower normalize to a reciprocal-square-root multiply; this is its correctly rounded form)
 __device__ __forceinline__ f3 normalize(f3 v) {

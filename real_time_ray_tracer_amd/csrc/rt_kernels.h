@@ -20,6 +20,7 @@ struct FrameParams {
   int spp, D, F, frame;
   int b1_min;                // AO: least live lanes of a prepared batch for its batched first bounce (set at launch)
   float inv_spp, fW, fH;     // 1.0f / spp, (float)W, (float)H: host-computed wave-uniform constants
+  float inv_W, inv_H;        // 1.0f / fW, 1.0f / fH (correctly rounded; div_rn_by)
   float hx, hy, hz;          // horizontal
   float vx, vy, vz;          // vertical
   float lx, ly, lz;          // llc_minus_campos

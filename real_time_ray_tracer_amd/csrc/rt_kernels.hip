@@ -120,6 +120,7 @@ __device__ __forceinline__ void store_color(const FrameParams& P, int x, int y, 
 // float-error margin has a computed discriminant < 0 for every lane (-1 in the reference,
 // never accepted) and is skipped.
 // ---------------------------------------------------------------------------------------
+constexpr float kInv6 = 1.0f / 6.0f;  // correctly rounded (div_rn_by)
 constexpr int kPool = 256;
 constexpr int kSetupCost = 24;
 constexpr int kTailMaxObj = 128;  // split tail rounds stage the sphere table in LDS up to this size  // per-sample setup (hashes, directions, shading) in sphere-test units
@@ -351,7 +352,7 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
   tile_xy(x, y, P.trace_row0);
   const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
   const f3 cam = mk(P.cx, P.cy, P.cz), light = mk(P.Lx, P.Ly, P.Lz);
-  const f3 dir = primary_dir(P, (float)x / P.fW, (float)y / P.fH);
+  const f3 dir = primary_dir(P, div_rn_by((float)x, P.fW, P.inv_W), div_rn_by((float)y, P.fH, P.inv_H));
   float t;
   int ind;
   if (ALLSPH) {
@@ -406,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
   const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
   const f3 light = mk(P.Lx, P.Ly, P.Lz);
   f3 pos = mk(P.cx, P.cy, P.cz);
-  f3 dir = primary_dir(P, (float)x / P.fW, (float)y / P.fH);
+  f3 dir = primary_dir(P, div_rn_by((float)x, P.fW, P.inv_W), div_rn_by((float)y, P.fH, P.inv_H));
   float arefl = 0.0f;          // array[2].w
   float rr = 0, rg = 0, rb = 0;  // result_color.rgb
   float c = 0.0f;
@@ -515,17 +516,17 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4*
     const float4* rbuf = P.rb;
     float hp, vp;
     if (aa == 0) {
-      hp = px / (float)P.W;
-      vp = py / (float)P.H;
+      hp = div_rn_by(px, P.fW, P.inv_W);
+      vp = div_rn_by(py, P.fH, P.inv_H);
     } else {  // jitter, ao_compute.glsl:310-323
       float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
       float u = grandom(((s.x + px * f.z) - px) + f.x, ((f.y + py * s.w) - py) + s.y);
       float w = grandom(s.z * px - (f.x * px) * f.z, f.w * py - (s.y * py) * s.w);
       normalize2(u, w);
-      float jx = u / 6.0f - 0.08333f;
-      float jy = w / 6.0f - 0.08333f;
-      hp = (px + jx) / (float)P.W;
-      vp = (py + jy) / (float)P.H;
+      float jx = div_rn_by(u, 6.0f, kInv6) - 0.08333f;
+      float jy = div_rn_by(w, 6.0f, kInv6) - 0.08333f;
+      hp = div_rn_by(px + jx, P.fW, P.inv_W);
+      vp = div_rn_by(py + jy, P.fH, P.inv_H);
     }
     f3 dir = primary_dir(P, hp, vp);
     // get_pt_within_unit_sphere(aa): depends on (aa, pixel) only -> hoisted out of the bounce loop
@@ -836,10 +837,10 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         float u = grandom(((s.x + px * f.z) - px) + f.x, ((f.y + py * s.w) - py) + s.y);
         float w = grandom(s.z * px - (f.x * px) * f.z, f.w * py - (s.y * py) * s.w);
         normalize2(u, w);
-        const float jx = aa == 0 ? 0.0f : u / 6.0f - 0.08333f;
-        const float jy = aa == 0 ? 0.0f : w / 6.0f - 0.08333f;
-        hp = (px + jx) / P.fW;
-        vp = (py + jy) / P.fH;
+        const float jx = aa == 0 ? 0.0f : div_rn_by(u, 6.0f, kInv6) - 0.08333f;
+        const float jy = aa == 0 ? 0.0f : div_rn_by(w, 6.0f, kInv6) - 0.08333f;
+        hp = div_rn_by(px + jx, P.fW, P.inv_W);
+        vp = div_rn_by(py + jy, P.fH, P.inv_H);
       }
       bdir = primary_dir(P, hp, vp);
       // get_pt_within_unit_sphere(aa), hoisted: it depends on aa and the pixel only, so it is
@@ -1312,10 +1313,10 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
         float u = grandom(((sv.x + px * f.z) - px) + f.x, ((f.y + py * sv.w) - py) + sv.y);
         float w = grandom(sv.z * px - (f.x * px) * f.z, f.w * py - (sv.y * py) * sv.w);
         normalize2(u, w);
-        const float jx = aa == 0 ? 0.0f : u / 6.0f - 0.08333f;
-        const float jy = aa == 0 ? 0.0f : w / 6.0f - 0.08333f;
-        hp = (px + jx) / P.fW;
-        vp = (py + jy) / P.fH;
+        const float jx = aa == 0 ? 0.0f : div_rn_by(u, 6.0f, kInv6) - 0.08333f;
+        const float jy = aa == 0 ? 0.0f : div_rn_by(w, 6.0f, kInv6) - 0.08333f;
+        hp = div_rn_by(px + jx, P.fW, P.inv_W);
+        vp = div_rn_by(py + jy, P.fH, P.inv_H);
       }
       bdir = primary_dir(P, hp, vp);
       bpos = cam;

@@ -231,7 +231,9 @@ void fill_params(const rt_ctx* c, int frame, rt::FrameParams& p) {
   p.spp = c->cfg.spp;
   p.inv_spp = 1.0f / (float)c->cfg.spp;
   p.fW = (float)c->cfg.width;
+  p.inv_W = 1.0f / p.fW;
   p.fH = (float)c->cfg.height;
+  p.inv_H = 1.0f / p.fH;
   p.D = c->cfg.max_depth;
   p.F = c->cfg.num_frames;
   p.frame = frame;
