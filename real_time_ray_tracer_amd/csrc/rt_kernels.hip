@@ -232,6 +232,28 @@ __device__ __forceinline__ bool bounce_cone_misses(const ConeB& c, float4 g) {
   return cphi < K;  // (2)
 }
 
+// bounce_cone_misses plus the sphere's per-ray pre-test for the batch: with theta = 0 (the
+// cone of ONE ray, around its own direction d) the same argument shows that a live lane
+// whose direction has dot(d, (c - o) / |c - o|) < cos(alpha) - 2e-5 cannot accept the sphere
+// (|d| = 1 within 3e-7 and u's fast-math error is ~1e-7, both far inside the 2e-5 slack).
+// pt = (u, K) with K = cos(alpha) - 2e-5, or K = -2 (every lane tests) when (1) fails.
+__device__ __forceinline__ bool bounce_cone_keep_pt(const ConeB& c, float4 g, float4& pt) {
+  const float vx = g.x - c.ox, vy = g.y - c.oy, vz = g.z - c.oz;
+  const float L = fast_sqrt(vx * vx + vy * vy + vz * vz);
+  const float r = fabsf(g.w), Lmax = L + c.rho;
+  pt = make_float4(0.0f, 0.0f, 0.0f, -2.0f);
+  if (!((L - c.rho - r) > 1e-2f * Lmax)) return true;  // (1)
+  const float R = fast_sqrt(r * r + 1e-5f * (Lmax * Lmax + r * r)) * 1.00001f + c.rho;
+  const float il = fast_rcp(L);
+  const float sa = R * il, ca = fast_sqrt(fmaxf(0.0f, 1.0f - sa * sa));
+  const float ux = vx * il, uy = vy * il, uz = vz * il;
+  if (sa < 1.0f) pt = make_float4(ux, uy, uz, ca - 2e-5f);
+  if (!(c.st * ca + c.ct * sa > 1e-5f)) return true;
+  const float K = c.ct * ca - c.st * sa - 2e-5f;
+  const float cphi = c.ax * ux + c.ay * uy + c.az * uz;
+  return !(cphi < K);  // (2)
+}
+
 // Closest hit of the camera rays of a pixel rectangle whose cone is `cone`: per 64-sphere
 // word the wave culls the spheres lane-parallel, then tests the survivors in ascending index
 // order, reading them on the scalar path (wave-uniform index).  Same result as closest_hit.
@@ -645,8 +667,11 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
 }
 
 template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
-          int SPPC = 0>
+          int SPPC = 0, bool PT = false, bool CNT = true>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
+  // CNT = false: the work counters compiled out (timed launches pass none): fewer live scalars
+  unsigned long long* const cnts = CNT ? P.counters : nullptr;
+  unsigned long long* const rowc = CNT ? P.row_counters : nullptr;
   extern __shared__ float4 lds[];
   const int spp = SPPC ? SPPC : P.spp, W = P.W, D = P.D, nobj = P.nobj;
   const int TP = POOL / spp > 0 ? POOL / spp : 1;
@@ -666,8 +691,14 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   // TAIL: the sphere table in LDS (per-lane sphere indices in the split tail rounds)
   float4* geol = (float4*)(lbase + LO.geol);  // [nobj] when TAIL && nobj <= kTailMaxObj
   const bool tail_ok = TAIL && nobj <= kTailMaxObj;
-  if (tail_ok)
+  // PT: the batched first bounce keeps its per-ray pre-test table in the same LDS rows, so the
+  // sphere table is (re)staged only when a split tail round needs it
+  const bool pt_ok = PT && B1 && tail_ok;
+  bool geol_valid = false;  // wave-uniform
+  if (tail_ok && !pt_ok) {
     for (int k = lane; k < nobj; k += 64) geol[k] = geo[k];
+    geol_valid = true;
+  }
   const float4* col = P.shapes + 2 * P.S;
   const float4* aux = P.shapes + 3 * P.S;
 
@@ -733,10 +764,10 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       P.nrm[off] = z;
       P.dep[off] = z;  // (0, 0, 0, 0) / AA
       store_color(P, x, y, col);
-      if (P.row_counters) atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)spp);  // ~free
+      if (rowc) atomicAdd(&rowc[y - P.band_row0], (unsigned long long)spp);  // ~free
     }
-    if (P.counters && lane == 0) {
-      unsigned long long* c = P.counters + (blockIdx.x & (kCounterSlots - 1));
+    if (cnts && lane == 0) {
+      unsigned long long* c = cnts + (blockIdx.x & (kCounterSlots - 1));
       atomicAdd(&c[0 * kCounterSlots], (unsigned long long)total);
       atomicAdd(&c[1 * kCounterSlots], (unsigned long long)total);
       atomicAdd(&c[3 * kCounterSlots], (unsigned long long)total * (unsigned long long)nobj);
@@ -772,10 +803,10 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       const int lq = div_spp(it);
       atomicMax(&pstop[lq], ((it - lq * spp) << 16) | (int)stopv);
     }
-    if (P.row_counters) {
+    if (rowc) {
       int x, y;
       pool_xy(div_spp(it), x, y);
-      atomicAdd(&P.row_counters[y - P.band_row0],
+      atomicAdd(&rowc[y - P.band_row0],
                 (unsigned long long)(kSetupCost + ncull + (segs >= 2 ? b1cost + (segs - 2) * nobj : 0)));
     }
   };
@@ -894,19 +925,39 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         b1cost = 0;
         for (int w = 0; w < nwords; ++w) {
           const int i = (w << 6) + lane;
-          const bool keep = i < nobj && !bounce_cone_misses(cb, geo[i]);
+          bool keep;
+          if (pt_ok) {
+            float4 pt;
+            keep = i < nobj && bounce_cone_keep_pt(cb, geo[i], pt);
+            if (i < nobj) geol[i] = pt;
+          } else {
+            keep = i < nobj && !bounce_cone_misses(cb, geo[i]);
+          }
           unsigned long long m = __ballot(keep);
           m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
               (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
           exec_tests += (unsigned long long)__popcll(m);
           b1cost += __popcll(m);
           if (ABL == 3) tsec[6] += (unsigned long long)__popcll(m) << 24;  // sections: first-bounce survivors
-          if (live)
+          if (pt_ok) {
+            geol_valid = false;
+            __syncthreads();  // the pre-test rows are written
+            if (live)
+              while (m) {
+                const int k = (w << 6) + __builtin_ctzll(m);
+                m &= m - 1;
+                const float4 q = geol[k];  // wave-uniform address: LDS broadcast
+                const float4 g = geo[k];
+                if (fmaf(bdir.z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w)
+                  sphere_candidate(bpos, bdir, g, k, 0.0001f, t, ind);
+              }
+          } else if (live) {
             while (m) {
               const int k = (w << 6) + __builtin_ctzll(m);
               m &= m - 1;
               sphere_candidate(bpos, bdir, geo[k], k, 0.0001f, t, ind);
             }
+          }
         }
         if (live) {
           ++nseg;
@@ -967,6 +1018,11 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     // lowest index on ties = exactly the sequential scan's result (ao_compute.glsl:183-194).
     const int L = __popcll(hm);
     if (tail_ok && next >= total && cursor >= nlive && L <= 32) {
+      if (!geol_valid) {
+        __syncthreads();
+        for (int k = lane; k < nobj; k += 64) geol[k] = geo[k];
+        geol_valid = true;
+      }
       int c = 0;
       while ((1 << c) < L) ++c;
       const int G = 64 >> c;  // the largest power of 2 with G * L <= 64
@@ -1019,10 +1075,10 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   }
   lap(2);
 
-  if (P.counters && ABL != 3) {
+  if (cnts && ABL != 3) {
     unsigned sg = wave_sum(nseg);
     if (lane == 0) {
-      unsigned long long* c = P.counters + (blockIdx.x & (kCounterSlots - 1));
+      unsigned long long* c = cnts + (blockIdx.x & (kCounterSlots - 1));
       atomicAdd(&c[0 * kCounterSlots], (unsigned long long)total);
       atomicAdd(&c[1 * kCounterSlots], (unsigned long long)sg);
       atomicAdd(&c[3 * kCounterSlots], (unsigned long long)sg * (unsigned long long)nobj);
@@ -1063,9 +1119,9 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     P.dep[off] = d;
     store_color(P, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
   }
-  if (ABL == 3 && P.counters && lane == 0) {
+  if (ABL == 3 && cnts && lane == 0) {
     lap(4);
-    unsigned long long* c = P.counters + (blockIdx.x & (kCounterSlots - 1));
+    unsigned long long* c = cnts + (blockIdx.x & (kCounterSlots - 1));
     for (int k = 0; k < 8; ++k) atomicAdd(&c[k * kCounterSlots], tsec[k]);
   }
 }
@@ -1578,6 +1634,20 @@ size_t shapes_lds_bytes(const FrameParams& p) { return (size_t)4 * p.nobj * size
 
 }  // namespace
 
+// The default pooled AO kernel (variant 7): with split tail rounds and the per-ray first-bounce
+// pre-test when the sphere table fits in LDS (tl), with or without the work counters.
+template <int SPPC>
+void launch_batch7(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStream_t stream, const FrameParams& q) {
+  if (tl && cnt)
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, true>), g, b, lds, stream, q, q.shapes);
+  else if (tl)
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false>), g, b, lds, stream, q, q.shapes);
+  else if (cnt)
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, SPPC, false, true>), g, b, lds, stream, q, q.shapes);
+  else
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, SPPC, false, false>), g, b, lds, stream, q, q.shapes);
+}
+
 hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, hipStream_t stream) {
   if (p.trace_rows <= 0) return hipSuccess;
   const size_t lds = shapes_lds_bytes(p);
@@ -1598,32 +1668,30 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
     const char* eb = getenv("RTRT_B1_MIN");
     FrameParams q = p;
     q.b1_min = eb ? atoi(eb) : 1;
-    if (all_spheres && (variant == 7 || variant == 27 || variant == 17 || variant == 11 || (variant >= 91 && variant <= 93))) {
+    if (all_spheres && (variant == 7 || variant == 9 || variant == 27 || variant == 17 || variant == 11 || (variant >= 91 && variant <= 93))) {
       const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
       const long long pools = (npix + TP - 1) / TP;
       const size_t psh = (size_t)batch_lds(p.spp, kPool,
-                                           (variant == 7 || variant == 27 || variant == 93) && p.nobj <= kTailMaxObj
+                                           (variant == 7 || variant == 9 || variant == 27 || variant == 93) && p.nobj <= kTailMaxObj
                                                ? p.nobj : 0).total;
       const dim3 g((unsigned)pools), b(64);
-      // spp 4, 16 and 64 (the reference's own scene, configs c/d, config e) have their own
-      // instantiations: constant LDS offsets and it / spp, fewer scalar registers (-5%)
       const bool tl = p.nobj <= kTailMaxObj;
-      if (variant == 7 && p.spp == 16 && tl)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 16>), g, b, psh, stream, q, p.shapes);
-      else if (variant == 7 && p.spp == 16)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, 16>), g, b, psh, stream, q, p.shapes);
-      else if (variant == 7 && p.spp == 64 && tl)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 64>), g, b, psh, stream, q, p.shapes);
+      // timed launches pass no counters: the counter code is compiled out (fewer live scalars)
+      const bool cnt = p.counters || p.row_counters;
+      // spp 4, 16 and 64 (the reference's own scene, configs c/d, config e) have their own
+      // instantiations: constant LDS offsets and it / spp, fewer scalar registers
+      if (variant == 7 && p.spp == 16)
+        launch_batch7<16>(tl, cnt, g, b, psh, stream, q);
       else if (variant == 7 && p.spp == 64)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, 64>), g, b, psh, stream, q, p.shapes);
-      else if (variant == 7 && p.spp == 4 && tl)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 4>), g, b, psh, stream, q, p.shapes);
+        launch_batch7<64>(tl, cnt, g, b, psh, stream, q);
       else if (variant == 7 && p.spp == 4)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, 4>), g, b, psh, stream, q, p.shapes);
-      else if (variant == 7 && tl)  // split tail rounds (the sphere table fits in LDS)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true>), g, b, psh, stream, q, p.shapes);
+        launch_batch7<4>(tl, cnt, g, b, psh, stream, q);
       else if (variant == 7)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true>), g, b, psh, stream, q, p.shapes);
+        launch_batch7<0>(tl, cnt, g, b, psh, stream, q);
+      else if (variant == 9 && p.spp == 16 && tl && !cnt)  // 7 without the per-ray first-bounce pre-test (A/B)
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 16, false, false>), g, b, psh, stream, q, p.shapes);
+      else if (variant == 9 && p.spp == 16 && tl)
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 16>), g, b, psh, stream, q, p.shapes);
       else if (variant == 27 && p.nobj <= kTailMaxObj)  // 7 without the batched first bounce (A/B)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true>), g, b, psh, stream, p, p.shapes);
       else if (variant == 11)

@@ -71,7 +71,7 @@ def test_full_size_band_parity(cfg, frames, rows):
     r.close()
 
 
-@pytest.mark.parametrize("variant", ["0", "2", "11", "17", "20", "25"])
+@pytest.mark.parametrize("variant", ["0", "2", "9", "11", "17", "20", "25"])
 def test_fallback_ao_kernels_match_oracle(variant, monkeypatch):
     """The other AO kernels agree too: the simple lane-per-sample ones (used for scenes with
     planes, or forced: 0, 2), the pooled kernel without lazy shortcuts (11) and the streaming
