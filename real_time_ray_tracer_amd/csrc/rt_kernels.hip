@@ -129,6 +129,13 @@ constexpr int kTailMaxObj = 128;  // split tail rounds stage the sphere table in
 // with inflated radius r_eff (r_eff^2 = r^2 + 1e-5 (d^2 + r^2)) lies outside the forward and
 // the backward cone iff |cos phi| < cos(theta + alpha), sin alpha = r_eff / d.  Float error
 // (~1e-6) is covered by the 2e-5 slack on the cosine and the 1e-5 inflation.
+// threadIdx.x & 63 recomputed at the point of use (volatile: not hoisted or shared)
+__device__ __forceinline__ int lane_id_here() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 struct ConeF {
   float ax, ay, az, ct, st;
 };
@@ -924,7 +931,9 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         int ind = -1;
         b1cost = 0;
         for (int w = 0; w < nwords; ++w) {
-          const int i = (w << 6) + lane;
+          // the lane index re-read here (not the kernel-wide one): otherwise the compiler keeps
+          // this loop's per-lane addresses live across the whole pool and spills them to scratch
+          const int i = (w << 6) + lane_id_here();
           bool keep;
           if (pt_ok) {
             float4 pt;
@@ -1020,7 +1029,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     if (tail_ok && next >= total && cursor >= nlive && L <= 32) {
       if (!geol_valid) {
         __syncthreads();
-        for (int k = lane; k < nobj; k += 64) geol[k] = geo[k];
+        for (int k = lane_id_here(); k < nobj; k += 64) geol[k] = geo[k];
         geol_valid = true;
       }
       int c = 0;
