@@ -166,23 +166,39 @@ def main():
     bounds = equal_bounds(H, world)
     balance_info = None
     if world > 1 and not args.no_balance:
+        piped = mode == 1 and not args.no_pipeline
+
         def strip_run(bnd, frames, counters):
+            """counters: one frame's row-counter profile.  Otherwise the strip's time per frame as
+            the timed run will render it: pipelined mode 1 by wall clock over 16 frames after 8,
+            else the kernels' HIP-event times of the last 3 of `frames` frames."""
             r = Renderer(W, H, S, spp, device=gpu, rows=(bnd[rank], bnd[rank + 1]))
             r.set_stream(stream)
             if counters:
                 r.enable_counters(totals=False, rows=True)
+            timed_wall = piped and not counters
+            if timed_wall:
+                r.enable_pipelining(True)
+                frames = 24
             f = 0
+            t0 = 0.0
             for k in range(frames):
                 header.fill_rand_buffer(7000 + k) if mode in (1, 2) else header.moving_light(False)
                 header.set_mode(f, S)
                 r.upload_header(header)
-                if k == frames - 3 and not counters:  # time the last 3 frames
+                if timed_wall and k == 8:
+                    r.synchronize()
+                    t0 = time.perf_counter()
+                if k == frames - 3 and not counters and not timed_wall:  # time the last 3 frames
                     r.enable_timing(True)
                     r.reset_stats()
                 f = r.dispatch(mode, f)
             out = r.read_row_counters().astype(np.float64) if counters else None
             ms = 0.0
-            if not counters:
+            if timed_wall:
+                r.synchronize()
+                ms = (time.perf_counter() - t0) / (frames - 8) * 1e3
+            elif not counters:
                 for p in {1: [1, 2], 2: [3], 3: [4], 4: [5]}[mode]:
                     n_l, tot = r.kernel_stats(p)
                     ms += tot / max(n_l, 1)
@@ -275,14 +291,19 @@ def main():
     torch.cuda.synchronize()
 
     # ---- timed region -----------------------------------------------------------------------
-    rend.enable_timing(True)
+    # per-launch HIP events only where the timed launches are the kernel durations (sequential);
+    # pipelined, the roofline uses the standalone launches below and the events are host cost
+    rend.enable_timing(not pipeline)
     rend.reset_stats()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host_s = 0.0  # host time inside step() (enqueue): the frame is host-bound if this nears elapsed
     for k in range(args.warmup, args.warmup + args.steps):
+        th = time.perf_counter()
         step(k)
+        host_s += time.perf_counter() - th
     if gather is not None:
         gather.finish()
     torch.cuda.synchronize()
@@ -319,10 +340,12 @@ def main():
     rend.enable_counters(False)
 
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    host_max = torch.tensor([host_s], dtype=torch.float64, device=cdev)
     strip_ms = torch.zeros(world, dtype=torch.float64, device=cdev)
     strip_ms[rank] = sum(tot / max(n_l, 1) for n_l, tot in solo.values())  # standalone kernel ms
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(host_max, op=dist.ReduceOp.MAX)
         dist.all_reduce(strip_ms)
     elapsed = float(t_max.item())
 
@@ -356,7 +379,7 @@ def main():
             "kernel_ms": round(avg_ms, 4),
             "kernel_ms_measured": ("standalone launches (2 frames after the timed region); timed launches overlap"
                                    if pipeline else "timed region"),
-            "kernel_ms_timed_span": round(timed_ms, 4),
+            "kernel_ms_timed_span": None if pipeline else round(timed_ms, 4),
             "sustained_tflops_per_frame": round(sustained, 2),
             "flop_per_launch": FLOP_PER_TEST * tests,
             "tests_per_launch": tests,
@@ -378,6 +401,7 @@ def main():
                        + (", pipelined frames: consecutive AO passes on 2 alternating streams, post-process on a 3rd"
                           if pipeline else "")},
             "roofline": roof,
+            "host_ms_per_step": round(float(host_max.item()) / args.steps * 1e3, 4),
         }
         if balance_info is not None:
             sm = strip_ms.cpu().tolist()

@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--kernels", action="store_true", help="sum of kernel times (sequential) instead of frame wall time")
     ap.add_argument("--only", type=int, default=-1, help="time only this strip (e.g. under rocprofv3)")
     ap.add_argument("--calibrate", action="store_true",
-                    help="bench.py's calibration: time the plan's strips (kernel sums), rescale the profile, "
+                    help="bench.py's calibration: time the plan's strips (pipelined frames for mode 1), rescale the profile, "
                          "re-balance; best of three measured plans")
     a = ap.parse_args()
     W, H, S, spp, mode, _ = CONFIGS[a.config]
@@ -79,9 +79,9 @@ def main():
             from real_time_ray_tracer_amd.dist import calibrate_row_cost
             measured = []
             for it in range(3):
-                t = [frame_ms(W, H, S, spp, mode, h, (b[i], b[i + 1]), 3, warm=3, kernels=True) for i in range(a.n)]
+                t = [frame_ms(W, H, S, spp, mode, h, (b[i], b[i + 1]), 16, warm=8, kernels=mode != 1) for i in range(a.n)]
                 measured.append((max(t), list(b)))
-                print(f"calibration plan {it}: {b} kernel-sum ms {[round(x, 3) for x in t]}")
+                print(f"calibration plan {it}: {b} strip ms {[round(x, 3) for x in t]}")
                 if it < 2:
                     cost = calibrate_row_cost(b, cost, t)
                     b = balanced_bounds(cost, a.n)
