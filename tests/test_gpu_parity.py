@@ -83,6 +83,19 @@ def test_ao_spp_variants(spp):
     assert_bitwise(g.normals, s.normals, f"spp {spp} normals")
 
 
+@pytest.mark.parametrize("nobj", [64, 100, 128, 129, 200])
+def test_ao_scene_sizes(nobj):
+    """Sphere counts around the kernel's 64-sphere words and the 128-sphere LDS table limit
+    (split tail rounds + the first bounce's per-ray pre-test table up to 128, without above)."""
+    W, H = 48, 32
+    h = make_header(f"syn{nobj}", W, H, 16)
+    for mode in (1, 2):
+        g, s, img = run_both(h, W, H, mode, 2)
+        assert_close(g.image, img, f"{nobj} spheres mode {mode} image")
+        assert_bitwise(g.depth, s.depth, f"{nobj} spheres mode {mode} depth")
+        assert_bitwise(g.normals, s.normals, f"{nobj} spheres mode {mode} normals")
+
+
 @pytest.mark.parametrize("mode", [1, 4])
 def test_max_depth_variants(mode):
     W, H = 48, 32
