@@ -94,9 +94,12 @@ class StripPlan:
 
 
 class StripGather:
-    """Gathers every rank's [max_rows][W][4] image strip into rank 0 with torch.distributed
-    (RCCL on GPUs, gloo on CPU).  Strips are padded to max_rows so one gather moves them all;
-    with equal strips the gather lands directly in the frame tensor (no assembly copy)."""
+    """Gathers every rank's image strip into rank 0's [H][W][4] frame with point-to-point
+    transfers of exactly the strip's rows (torch.distributed batch_isend_irecv: grouped RCCL
+    send/recv on GPUs, gloo on CPU).  Strip r lands directly in rows [bounds[r], bounds[r+1])
+    of the frame, and rank 0 renders its own strip straight into its rows, so there is no
+    padding and no assembly copy (cost-balanced strips differ in height by up to ~3x, and a
+    padded gather would move max_rows for every rank)."""
 
     def __init__(self, plan: StripPlan, rank: int, device, nbuf: int = 2, root: int = 0, host_staging: bool = False):
         """host_staging: gather through host copies (gloo rehearsal of the GPU path)."""
@@ -105,48 +108,54 @@ class StripGather:
         self.plan, self.rank, self.root, self.nbuf = plan, rank, root, nbuf
         self.host_staging = host_staging
         self.device = device
-        R, W = plan.max_rows, plan.W
-        self.equal = all(plan.bounds[i + 1] - plan.bounds[i] == R for i in range(plan.n))
-        self.strips = [torch.zeros((R, W, 4), dtype=torch.float32, device=device) for _ in range(nbuf)]
-        self.frames = []
-        self.lists = []
+        W = plan.W
+        r0, r1 = plan.rows(rank)
         fdev = "cpu" if host_staging else device
+        self.frames = []
         if rank == root:
-            for _ in range(nbuf):
-                frame = torch.zeros((plan.n * R, W, 4), dtype=torch.float32, device=fdev)
-                self.frames.append(frame)
-                self.lists.append(list(frame.split(R, 0)))
+            self.frames = [torch.zeros((plan.H, W, 4), dtype=torch.float32, device=fdev) for _ in range(nbuf)]
+        if rank == root and not host_staging:
+            self.strips = [f[r0:r1] for f in self.frames]  # contiguous rows of the frame
+        else:
+            self.strips = [torch.zeros((r1 - r0, W, 4), dtype=torch.float32, device=device) for _ in range(nbuf)]
         self.pending = [None] * nbuf
 
     def strip(self, k: int):
         """Image buffer frame k renders into (waits for the gather that last used it)."""
         i = k % self.nbuf
-        if self.pending[i] is not None:
-            self.pending[i].wait()
-            self.pending[i] = None
+        self._wait(i)
         return self.strips[i]
 
-    def gather(self, k: int, async_op: bool = True):
+    def _wait(self, i: int):
+        if self.pending[i] is not None:
+            for w in self.pending[i]:
+                w.wait()
+            self.pending[i] = None
+
+    def gather(self, k: int):
         import torch.distributed as dist
 
         i = k % self.nbuf
-        lst = self.lists[i] if self.rank == self.root else None
-        src = self.strips[i].cpu() if self.host_staging else self.strips[i]
-        work = dist.gather(src, gather_list=lst, dst=self.root, async_op=async_op)
-        if async_op:
-            self.pending[i] = work
+        ops = []
+        if self.rank == self.root:
+            if self.host_staging:  # rank 0's own strip into the host frame
+                r0, r1 = self.plan.rows(self.rank)
+                self.frames[i][r0:r1].copy_(self.strips[i].cpu())
+            for r in range(self.plan.n):
+                if r != self.root:
+                    a, b = self.plan.rows(r)
+                    ops.append(dist.P2POp(dist.irecv, self.frames[i][a:b], r))
+        else:
+            src = self.strips[i].cpu() if self.host_staging else self.strips[i]
+            ops.append(dist.P2POp(dist.isend, src, self.root))
+        self.pending[i] = dist.batch_isend_irecv(ops) if ops else None
 
     def finish(self):
-        for i, w in enumerate(self.pending):
-            if w is not None:
-                w.wait()
-                self.pending[i] = None
+        for i in range(self.nbuf):
+            self._wait(i)
 
     def frame(self, k: int):
-        """Rank 0: the assembled [H][W][4] frame of frame k (after finish())."""
+        """Rank 0: the [H][W][4] frame of frame k (after finish())."""
         if self.rank != self.root:
             return None
-        full = self.frames[k % self.nbuf]
-        if self.equal:
-            return full
-        return self.plan.assemble(self.lists[k % self.nbuf])
+        return self.frames[k % self.nbuf]
