@@ -1710,7 +1710,7 @@ hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, h
       else if (variant == 92)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2>), g, b, psh, stream, p, p.shapes);
       else if (variant == 93 && p.nobj <= kTailMaxObj && p.spp == 16)  // section clocks of variant 7
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true, 16>), g, b, psh, stream, q, p.shapes);
+        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true, 16, true>), g, b, psh, stream, q, p.shapes);
       else if (variant == 93 && p.nobj <= kTailMaxObj)
         hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true>), g, b, psh, stream, q, p.shapes);
       else if (variant == 93)
