@@ -48,7 +48,10 @@ def det_sin(x):
     r = fma(-k, F(1.57079637), x)
     r = fma(-k, F(-4.37113883e-08), r)
     r = fma(-k, F(-1.71512451e-15), r)
-    q = (k - F(4.0) * np.floor(k * F(0.25))).astype(np.int64)
+    # quadrant: integer k mod 4, k converted as v_cvt_i32_f32 (saturating beyond 2^31)
+    kf = np.where(np.isfinite(k), k, F(0.0)).astype(np.float64)
+    ki = np.clip(kf, -2.0 ** 31, 2.0 ** 31 - 1).astype(np.int64)
+    q = ki & 3
     z = r * r
     s = fma(r * z, fma(z, fma(z, F(-1.9515295891e-4), F(8.3321608736e-3)), F(-1.6666654611e-1)), r)
     c = fma(z * z, fma(z, fma(z, F(2.443315711809948e-5), F(-1.388731625493765e-3)), F(4.166664568298827e-2)),

@@ -14,6 +14,7 @@
 #include "rt_oracle.h"
 
 #include <math.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -56,8 +57,10 @@ float rto_sin(float x) {
   float r = fmaf(-k, 1.57079637f, x);
   r = fmaf(-k, -4.37113883e-08f, r);
   r = fmaf(-k, -1.71512451e-15f, r);
-  float q4 = k - 4.0f * floorf(k * 0.25f); /* k mod 4, exact for |k| < 2^24 */
-  int q = (int)q4;
+  /* quadrant: the integer k mod 4, with k converted as v_cvt_i32_f32 does (saturating beyond
+     2^31, where the quadrant is 3 for +k and 0 for -k); exact k mod 4 for |k| < 2^31 */
+  int32_t ki = k >= 2147483648.0f ? INT32_MAX : (k < -2147483648.0f ? INT32_MIN : (int32_t)k);
+  int q = (int)((uint32_t)ki & 3u);
   float z = r * r;
   float s = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
   float c = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),

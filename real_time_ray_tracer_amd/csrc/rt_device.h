@@ -82,13 +82,15 @@ __device__ __forceinline__ float det_sin(float x) {
   float r = fmaf(-k, 1.57079637f, x);
   r = fmaf(-k, -4.37113883e-08f, r);
   r = fmaf(-k, -1.71512451e-15f, r);
-  float q4 = k - 4.0f * floorf(k * 0.25f);
-  int q = (int)q4;
+  // quadrant q = k mod 4 from the integer k (v_cvt_i32_f32 saturates beyond 2^31; the oracle
+  // mirrors that): bit 0 picks cos, bit 1 flips the sign, both read from k << 30
+  const unsigned qs = (unsigned)(int)k << 30;
   float z = r * r;
   float s = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
   float c = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
                  fmaf(-0.5f, z, 1.0f));
-  return (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
+  const float v = (qs & 0x40000000u) ? c : s;
+  return __uint_as_float(__float_as_uint(v) ^ (qs & 0x80000000u));
 }
 
 // IEEE binary32 square root, correctly rounded: the value sqrtf() has under
@@ -229,7 +231,10 @@ __device__ __forceinline__ void sphere_candidate(f3 pos, f3 dir, float4 g, int i
     float t1 = -1.0f * b + s;
     float t2 = -1.0f * b - s;
     float res = (t2 < 0.0f) ? t1 : t2;
-    const bool acc = (res > thr) & ((res < t) | (t < 0.0f));  // no short-circuit branches
+    // (res < t || t < 0) as one unsigned compare: t is -1.0f (no hit yet, bits 0xBF800000, above
+    // every positive float's bits, +inf included) or an accepted res > thr >= 0; for res > thr
+    // (positive, not NaN) and positive t the float and bit orders agree
+    const bool acc = (res > thr) & (__float_as_uint(res) < __float_as_uint(t));  // no short-circuit branches
     t = acc ? res : t;
     ind = acc ? i : ind;
   }
