@@ -230,7 +230,11 @@ __device__ __forceinline__ void sphere_candidate(f3 pos, f3 dir, float4 g, int i
     float s = thr >= 1e-6f ? sqrt_rn_tail(del) : sqrt_rn(del);  // thr is a literal at every call
     float t1 = -1.0f * b + s;
     float t2 = -1.0f * b - s;
-    float res = (t2 < 0.0f) ? t1 : t2;
+    // (t2 < 0 ? t1 : t2) as an unsigned min of the bits: t1 >= t2, so for t2 >= 0 both are
+    // non-negative and the min is t2; a negative t2 has its sign bit set and loses to t1 >= 0;
+    // the remaining cases (both negative, or t2 = -0 with t1 = +0) give a value <= 0 either
+    // way, which the acceptance below rejects (thr >= 0)
+    float res = __uint_as_float(min(__float_as_uint(t1), __float_as_uint(t2)));
     // (res < t || t < 0) as one unsigned compare: t is -1.0f (no hit yet, bits 0xBF800000, above
     // every positive float's bits, +inf included) or an accepted res > thr >= 0; for res > thr
     // (positive, not NaN) and positive t the float and bit orders agree
