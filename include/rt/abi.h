@@ -165,10 +165,13 @@ enum {
   RT_MATH_SPHERE = 5,    /* sphere_eval_ray (in: pos3,dir3,center3,r = 10 floats)      */
   RT_MATH_SQRT_SWEEP = 6, /* out[i] = #bit patterns in [i*in[0], (i+1)*in[0]) of the
                              non-negative floats where the kernels' sqrt != sqrtf         */
-  RT_MATH_RCP_SWEEP = 7   /* out[i] = #bit patterns in [i*in[0], (i+1)*in[0]) of the non-
+  RT_MATH_RCP_SWEEP = 7,  /* out[i] = #bit patterns in [i*in[0], (i+1)*in[0]) of the non-
                              negative floats x where the kernels' 1/sqrt (normalize) differs
                              from 1.0f/sqrtf(x), plus those of the normal x in [2^-126, 2^126]
                              where their reciprocal differs from 1.0f/x                   */
+  RT_MATH_SQRT_TAIL_SWEEP = 8 /* out[i] = #bit patterns in [i*in[0], (i+1)*in[0]) of the finite
+                             non-negative floats where the hit-tail sqrt breaks its contract
+                             (== sqrtf on [2^-96, FLT_MAX], in [0, 2^-47] below)          */
 };
 int rt_selftest_math(rt_ctx* ctx, int fn, const float* in, float* out, size_t n);
 

@@ -25,13 +25,13 @@ __device__ __forceinline__ f3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
 __device__ __forceinline__ float dot(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 // 1 / sqrtf(d), correctly rounded twice (IEEE sqrt, then IEEE division), as the reference
 // semantics of normalize() (below).  When every active lane has d in [2^-96, 2^126) (always,
-// in practice) it is computed as sqrt_rn_tail (exact there) followed by v_rcp_f32 and one
+// in practice) it is computed as sqrt_rn_core (exact there) followed by v_rcp_f32 and one
 // Newton step, fma(fma(-s, y, 1), y, y): that step returns 1.0f / s exactly for every
 // normal s in [2^-126, 2^126] (checked on the device for all of them:
 // tests/test_gpu_parity.py::test_rcp_rn_exhaustive), and s lies in [2^-48, 2^63).  Other
 // inputs (0, tiny, huge, inf, NaN) take the compiler's sequence.  About 13 instructions
 // shorter than the division + scaled sqrt it replaces.
-__device__ __forceinline__ float sqrt_rn_tail(float x);
+__device__ __forceinline__ float sqrt_rn_core(float x);
 __device__ __forceinline__ float rcp_rn_normal(float s) {
   const float y = __builtin_amdgcn_rcpf(s);
   return fmaf(fmaf(-s, y, 1.0f), y, y);
@@ -39,7 +39,7 @@ __device__ __forceinline__ float rcp_rn_normal(float s) {
 __device__ __forceinline__ float inv_len_rn(float d) {
   // d in [2^-96, 2^126) as one unsigned compare on the bits (NaN and negatives fail)
   const bool ok = __float_as_uint(d) - 0x0F800000u < 0x7E800000u - 0x0F800000u;
-  if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) == 0, 1)) return rcp_rn_normal(sqrt_rn_tail(d));
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) == 0, 1)) return rcp_rn_normal(sqrt_rn_core(d));
   return 1.0f / sqrtf(d);
 }
 // a / b for a divisor b known ahead with y = 1.0f / b (correctly rounded): Markstein's
@@ -112,22 +112,27 @@ __device__ __forceinline__ float sqrt_rn(float x) {
   return tiny ? s * 0x1p-16f : s;
 }
 
-// sqrt_rn without the tiny-input scaling, for the hit tail of sphere_candidate when the
-// acceptance threshold is >= 1e-6.  Equal to sqrt_rn for x >= 2^-96.  Below that it returns
-// some value in [0, 2^-47] (v_sqrt may flush or approximate there), and no caller can tell:
-// with s < 2^-47 and |b| >= 2^-22, s is below a quarter ulp of b, so fl(-b + s) and
-// fl(-b - s) are both -b whatever s is; with |b| < 2^-22 both roots are below 2.4e-7 in
-// magnitude and never pass the threshold.  Accepted t and index are therefore unchanged.
-__device__ __forceinline__ float sqrt_rn_tail(float x) {
-  float s = __builtin_amdgcn_sqrtf(x);
-  const float sm = __int_as_float(__float_as_int(s) - 1);
-  const float sp = __int_as_float(__float_as_int(s) + 1);
-  const float rm = fmaf(-sm, s, x);
-  const float rp = fmaf(-sp, s, x);
-  s = (rm <= 0.0f) ? sm : s;
-  s = (rp > 0.0f) ? sp : s;
-  return s;
+// IEEE binary32 square root for x in [2^-96, FLT_MAX], from the reciprocal square root:
+// y = v_rsq_f32(x), g = x*y, h = y/2, r = fma(-g, g, x) (exact), s = fma(r, h, g) — Markstein's
+// correction step.  One transcendental and 4 VALU instead of v_sqrt_f32 + the 8-instruction
+// one-ulp fix-up.  Equal to sqrtf on EVERY float of that range (device sweep:
+// tests/test_gpu_parity.py::test_sqrt_tail_exhaustive, RT_MATH_SQRT_TAIL_SWEEP).  Outside it:
+// 0 gives NaN (0 * inf) and +inf gives NaN, so callers clamp or range-check.
+__device__ __forceinline__ float sqrt_rn_core(float x) {
+  const float y = __builtin_amdgcn_rsqf(x);
+  const float g = x * y, h = 0.5f * y;
+  return fmaf(fmaf(-g, g, x), h, g);
 }
+
+// sqrt_rn without the tiny-input scaling, for the hit tail of sphere_candidate when the
+// acceptance threshold is >= 1e-6: sqrt_rn_core of max(x, 2^-100).  Equal to sqrt_rn for x in
+// [2^-96, FLT_MAX].  Below 2^-96 it returns some value in [0, 2^-47] (checked by the same
+// sweep), and no caller can tell: with s < 2^-47 and |b| >= 2^-22, s is below a quarter ulp
+// of b, so fl(-b + s) and fl(-b - s) are both -b whatever s is; with |b| < 2^-22 both roots
+// are below 2.4e-7 in magnitude and never pass the threshold.  Accepted t and index are
+// therefore unchanged.  (x = +inf, a discriminant that overflowed — |b| > 2^64 — gives NaN,
+// which the caller rejects, where sqrt_rn gives +inf.)
+__device__ __forceinline__ float sqrt_rn_tail(float x) { return sqrt_rn_core(fmaxf(x, 0x1p-100f)); }
 
 // random(vec2), p_compute.glsl:65-75
 __device__ __forceinline__ float grandom(float sx, float sy) {

@@ -1624,6 +1624,20 @@ __global__ void selftest_kernel(int fn, const float* __restrict__ in, float* __r
       out[i] = (float)bad;
       break;
     }
+    case 8: {  // exhaustive sqrt_rn_tail contract over [0, 0x7f7fffff]: == sqrtf on [2^-96, FLT_MAX], in [0, 2^-47] below
+      const unsigned per = (unsigned)in[0];
+      unsigned bad = 0;
+      for (unsigned k = 0; k < per; ++k) {
+        unsigned long long u = (unsigned long long)i * per + k;
+        if (u > 0x7f7fffffull) break;
+        float x = __uint_as_float((unsigned)u);
+        const float s = sqrt_rn_tail(x);
+        if (u >= 0x0f800000ull) bad += __float_as_uint(s) != __float_as_uint(sqrtf(x));
+        else bad += !(s >= 0.0f && s <= 0x1p-47f);
+      }
+      out[i] = (float)bad;
+      break;
+    }
     case 3: out[i] = in[2 * i] / in[2 * i + 1]; break;
     case 4: {
       f3 v = normalize(mk(in[3 * i], in[3 * i + 1], in[3 * i + 2]));

@@ -219,6 +219,17 @@ def test_sqrt_rn_exhaustive():
     assert float(bad.sum()) == 0.0, f"{int(bad.sum())} mismatching inputs"
 
 
+def test_sqrt_tail_exhaustive():
+    """The sphere hit tail's sqrt (v_rsq_f32 + Markstein's correction) equals sqrtf on every
+    float in [2^-96, FLT_MAX] and stays in [0, 2^-47] below 2^-96, on the device."""
+    r = Renderer(8, 8, 1, 1)
+    per, n = 2048, 1 << 20
+    bad = r.selftest_math(_lib.RT_MATH_SQRT_TAIL_SWEEP, np.array([per], np.float32), n)
+    r.close()
+    assert n * per > 0x7f7fffff
+    assert float(bad.sum()) == 0.0, f"{int(bad.sum())} inputs break the contract"
+
+
 def test_rcp_rn_exhaustive():
     """normalize's 1/sqrt (sqrt_rn_tail + v_rcp_f32 + one Newton step, with the compiler's
     sequence for out-of-range inputs) equals 1.0f/sqrtf on every non-negative float, and the
