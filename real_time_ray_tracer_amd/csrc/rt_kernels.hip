@@ -1102,9 +1102,22 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     pool_xy(lp, x, y);
     float sr = 0.0f, sg = 0.0f, sb = 0.0f;
     const float* ps = sres + lp * spp;
+    if (SPPC % 4 == 0 && SPPC > 0) {
+      // spp a multiple of 4 (constant): the pixel's samples read 4 at a time (ds_read_b128;
+      // 16-byte aligned: lp * spp and NS are multiples of 4), summed in the same aa order
 #pragma unroll 1
-    for (int k = 0; k < spp; ++k) {
-      sr = sr + ps[k]; sg = sg + ps[NS + k]; sb = sb + ps[2 * NS + k];
+      for (int k = 0; k < SPPC; k += 4) {
+        const float4 a = *(const float4*)(ps + k), g = *(const float4*)(ps + NS + k),
+                     c = *(const float4*)(ps + 2 * NS + k);
+        sr = sr + a.x; sr = sr + a.y; sr = sr + a.z; sr = sr + a.w;
+        sg = sg + g.x; sg = sg + g.y; sg = sg + g.z; sg = sg + g.w;
+        sb = sb + c.x; sb = sb + c.y; sb = sb + c.z; sb = sb + c.w;
+      }
+    } else {
+#pragma unroll 1
+      for (int k = 0; k < spp; ++k) {
+        sr = sr + ps[k]; sg = sg + ps[NS + k]; sb = sb + ps[2 * NS + k];
+      }
     }
     const int st = pstop[lp];
     const float ystop = st < 0 ? -1.0f : (float)(st & 0xffff);
