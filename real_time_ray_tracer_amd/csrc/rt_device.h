@@ -132,7 +132,13 @@ __device__ __forceinline__ float sqrt_rn_core(float x) {
 // are below 2.4e-7 in magnitude and never pass the threshold.  Accepted t and index are
 // therefore unchanged.  (x = +inf, a discriminant that overflowed — |b| > 2^64 — gives NaN,
 // which the caller rejects, where sqrt_rn gives +inf.)
-__device__ __forceinline__ float sqrt_rn_tail(float x) { return sqrt_rn_core(fmaxf(x, 0x1p-100f)); }
+// (The clamp is one v_max_f32 written out: fmaxf adds a canonicalising v_max in front of it,
+// which buys nothing here, x being a non-negative discriminant and never NaN.)
+__device__ __forceinline__ float sqrt_rn_tail(float x) {
+  float xc;
+  asm("v_max_f32_e32 %0, 0x0d800000, %1" : "=v"(xc) : "v"(x));  // max(x, 2^-100)
+  return sqrt_rn_core(xc);
+}
 
 // random(vec2), p_compute.glsl:65-75
 __device__ __forceinline__ float grandom(float sx, float sy) {
