@@ -112,6 +112,15 @@ int rt_run_program(rt_ctx* ctx, int program, int frame);
  * mode 1 = aop_compute + aop_postprocessing, 2 = ao_compute, 3 = p_compute, 4 = h_compute.
  * Returns the next frame slot (frame+1) % num_frames, as compute_one_shader does. */
 int rt_dispatch(rt_ctx* ctx, int mode, int frame);
+/* n consecutive compute() calls (src/main.cpp:553-578) as the reference's render loop makes
+ * them (src/main.cpp:763-781), with the host-side updates in C++: per frame k = 0..n-1,
+ * fill_rand_buffer(rand_seed + k) for the AO modes (1, 2) or moving_light(light_movement) for
+ * the Phong modes (3, 4); set_mode(frame slot, int(mode.z)); upload the header; dispatch.
+ * header: the caller's std430 prefix (rt_header_bytes(S, spp) bytes), updated in place as the
+ * host loop leaves it.  Equal, frame for frame, to n rounds of those calls made one by one.
+ * Returns the next frame slot, or < 0. */
+int rt_compute_frames(rt_ctx* ctx, float* header, int mode, int frame, int n, uint64_t rand_seed,
+                      int light_movement);
 /* Copy device state to the host in the REFERENCE layout.  Any pointer may be NULL.
  * pixels/normals/depth: [F][W][R] vec4 (x-major, y fastest; R = rows of this context),
  * image: [R][W] rgba32f (row 0 = row_begin, bottom-left origin like the GL texture). */

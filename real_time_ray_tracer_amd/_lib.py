@@ -52,6 +52,7 @@ SIGNATURES = {
     "rt_upload_rand_buffer": (C.c_int, [_ctx, _fp, C.c_size_t]),
     "rt_run_program": (C.c_int, [_ctx, C.c_int, C.c_int]),
     "rt_dispatch": (C.c_int, [_ctx, C.c_int, C.c_int]),
+    "rt_compute_frames": (C.c_int, [_ctx, _fp, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int]),
     "rt_download": (C.c_int, [_ctx, _fp, _fp, _fp, _fp]),
     "rt_upload_gbuffer": (C.c_int, [_ctx, _fp, _fp, _fp]),
     "rt_image_device_ptr": (_vp, [_ctx]),

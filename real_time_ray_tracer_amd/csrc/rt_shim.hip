@@ -673,6 +673,26 @@ int rt_dispatch(rt_ctx* c, int mode, int frame) {
   return (frame + 1) % c->cfg.num_frames;
 }
 
+int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint64_t rand_seed, int light_movement) {
+  if (!c || !header || n < 0 || mode < RT_MODE_AO_PP || mode > RT_MODE_PHONG_REFL) return RT_E_INVAL;
+  const int S = c->cfg.num_shapes, spp = c->cfg.spp;
+  const size_t bytes = rt_header_bytes(S, spp);
+  for (int k = 0; k < n; ++k) {
+    int rc = (mode == RT_MODE_AO_PP || mode == RT_MODE_AO) ? rt_fill_rand_buffer(header, S, spp, rand_seed + (uint64_t)k)
+                                                           : rt_moving_light(header, light_movement);
+    if (rc != RT_OK) return rc;
+    const float mz = header[RT_HDR_MODE * 4 + 2];
+    if (!(mz >= 0.0f && mz < (float)(S + 1))) return RT_E_INVAL;
+    rc = rt_set_mode(header, frame, (int)mz);
+    if (rc != RT_OK) return rc;
+    rc = rt_upload_header(c, header, bytes);
+    if (rc != RT_OK) return rc;
+    frame = rt_dispatch(c, mode, frame);
+    if (frame < 0) return frame;
+  }
+  return frame;
+}
+
 int rt_download(rt_ctx* c, float* pixels, float* normals, float* depth, float* image) {
   if (!c) return RT_E_INVAL;
   RT_HIP(c, hipSetDevice(c->device));

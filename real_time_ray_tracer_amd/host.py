@@ -239,6 +239,14 @@ class Renderer:
     def dispatch(self, mode: int, frame: int) -> int:
         return self._c(self._lib.rt_dispatch(self.ctx, mode, frame), f"rt_dispatch(mode {mode})")
 
+    def compute_frames(self, header: Header, mode: int, frame: int, n: int, rand_seed: int = 7000,
+                       light_movement: bool = False) -> int:
+        """n compute() rounds with the per-frame host updates done in C++ (rt_compute_frames):
+        fill_rand_buffer(rand_seed + k) or moving_light, set_mode, upload, dispatch.  `header`
+        is updated in place as the frame loop leaves it.  Returns the next frame slot."""
+        return self._c(self._lib.rt_compute_frames(self.ctx, header._p(), mode, frame, n, rand_seed,
+                                                   int(bool(light_movement))), "rt_compute_frames")
+
     def download(self, pixels=True, normals=True, depth=True, image=True) -> GBuffer:
         shp = (self.F, self.W, self.R, 4)
         p = np.empty(shp, np.float32) if pixels else None
@@ -321,6 +329,13 @@ class FrameDriver:
         self.frame_num = 0
         self.frames_done = 0
         self.rand_seed0 = rand_seed0
+
+    def compute_many(self, n: int) -> int:
+        """n compute() calls in one C++ loop (rt_compute_frames): same frames, less host time."""
+        self.frame_num = self.r.compute_frames(self.h, self.lighting, self.frame_num, n,
+                                               self.rand_seed0 + self.frames_done, self.light_movement)
+        self.frames_done += n
+        return self.frame_num
 
     def compute(self) -> int:
         if self.lighting in (1, 2):

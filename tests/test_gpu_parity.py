@@ -73,6 +73,32 @@ def test_mode_parity_small(scene, mode):
     assert_bitwise(g.depth, s.depth, f"{scene} mode {mode} depth")
 
 
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+def test_compute_frames_equals_frame_by_frame(mode):
+    """rt_compute_frames (the C++ frame loop) renders the same frames as FrameDriver.compute()
+    called once per frame: g-buffer ring, image, frame slot and the updated header, bit for bit."""
+    W, H, spp = 48, 32, 4
+    h = make_header("syn16", W, H, spp)
+    outs = []
+    for many in (False, True):
+        r = Renderer(W, H, h.S, h.AA)
+        hh = h.copy()
+        drv = FrameDriver(r, hh, mode, light_movement=True)
+        if many:
+            drv.compute_many(2)
+            drv.compute_many(3)
+        else:
+            for _ in range(5):
+                drv.compute()
+        outs.append((r.download(), hh.data.copy(), drv.frame_num))
+        r.close()
+    (g0, h0, f0), (g1, h1, f1) = outs
+    assert f0 == f1 == 5
+    assert_bitwise(h1, h0, f"mode {mode} header")
+    for name in ("image", "pixels", "normals", "depth"):
+        assert_bitwise(getattr(g1, name), getattr(g0, name), f"mode {mode} {name}")
+
+
 @pytest.mark.parametrize("spp", [1, 3, 16, 64])
 def test_ao_spp_variants(spp):
     W, H = 40, 24
