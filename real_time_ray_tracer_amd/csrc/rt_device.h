@@ -170,6 +170,22 @@ __device__ __forceinline__ float sphere_eval(f3 pos, f3 dir, float4 g) {
   return t2;
 }
 
+// sphere_eval for shadow rays, whose result is only compared with 0.0001 (p_compute.glsl:
+// 145-166): the square root is sqrt_rn_tail, which by its contract (thr >= 1e-6) leaves every
+// t > 0.0001 decision and every accepted t unchanged.
+__device__ __forceinline__ float sphere_eval_shadow(f3 pos, f3 dir, float4 g) {
+  f3 pmc = pos - xyz(g);
+  float b = dot(dir, pmc);
+  float del = fmaf(g.w, g.w, fmaf(b, b, -dot(pmc, pmc)));
+  if (del < 0.0f) return -1.0f;
+  if (del == 0.0f) return -1.0f * b;
+  float s = sqrt_rn_tail(del);
+  float t1 = -1.0f * b + s;
+  float t2 = -1.0f * b - s;
+  if (t2 < 0.0f) return (t1 < 0.0f) ? -1.0f : t1;
+  return t2;
+}
+
 // plane_eval_ray, p_compute.glsl:111-119
 __device__ __forceinline__ float plane_eval(f3 pos, f3 dir, float4 g, float4 g2) {
   f3 n = xyz(g);
@@ -372,7 +388,7 @@ __device__ __forceinline__ bool shadow_lit(const float4* __restrict__ geo, const
   f3 np = pos + 0.01f * l;
   const double dlen = (double)len;
   for (int i = 0; i < nobj; ++i) {
-    float tf = ALLSPH ? sphere_eval(np, l, geo[i]) : eval_shape(np, l, geo[i], geo2[i]);
+    float tf = ALLSPH ? sphere_eval_shadow(np, l, geo[i]) : eval_shape(np, l, geo[i], geo2[i]);
     double t = (double)tf;
     if (t > (double)0.0001f) {
       double dx = t * (double)l.x, dy = t * (double)l.y, dz = t * (double)l.z;

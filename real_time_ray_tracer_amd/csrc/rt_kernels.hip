@@ -322,7 +322,7 @@ __device__ __forceinline__ bool shadow_lit_cone(const float4* __restrict__ geo, 
     bool lit = true;
     for (int k = 0; k < n; ++k) {
       if (need && lit) {
-        const double t = (double)sphere_eval(np, l, geo[k]);
+        const double t = (double)sphere_eval_shadow(np, l, geo[k]);
         if (t > (double)0.0001f) {
           const double dx = t * (double)l.x, dy = t * (double)l.y, dz = t * (double)l.z;
           if (sqrt(fma(dz, dz, fma(dy, dy, dx * dx))) < dlen) lit = false;
@@ -363,7 +363,7 @@ __device__ __forceinline__ bool shadow_lit_cone(const float4* __restrict__ geo, 
       const int k = w + __builtin_ctzll(m);
       m &= m - 1;
       if (need && lit) {
-        const double t = (double)sphere_eval(np, l, geo[k]);
+        const double t = (double)sphere_eval_shadow(np, l, geo[k]);
         if (t > (double)0.0001f) {
           const double dx = t * (double)l.x, dy = t * (double)l.y, dz = t * (double)l.z;
           if (sqrt(fma(dz, dz, fma(dy, dy, dx * dx))) < dlen) lit = false;
