@@ -675,6 +675,7 @@ int rt_dispatch(rt_ctx* c, int mode, int frame) {
 
 int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint64_t rand_seed, int light_movement) {
   if (!c || !header || n < 0 || mode < RT_MODE_AO_PP || mode > RT_MODE_PHONG_REFL) return RT_E_INVAL;
+  if (frame < 0 || frame >= c->cfg.num_frames) return RT_E_INVAL;
   const int S = c->cfg.num_shapes, spp = c->cfg.spp;
   const size_t bytes = rt_header_bytes(S, spp);
   for (int k = 0; k < n; ++k) {

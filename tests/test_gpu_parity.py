@@ -278,9 +278,18 @@ def test_errors_are_reported():
         r.dispatch(7, 0)
     with pytest.raises(_lib.RtError):
         r.dispatch(1, 8)
+    with pytest.raises(_lib.RtError):
+        r.compute_frames(h, 7, 0, 1)  # unknown mode
+    with pytest.raises(_lib.RtError):
+        r.compute_frames(h, 1, 8, 1)  # frame slot out of range
+    with pytest.raises(_lib.RtError):
+        r.compute_frames(h, 1, 0, -1)  # negative frame count
+    assert r.compute_frames(h, 3, 6, 0) == 6  # no frames: the slot is returned unchanged
     h.set_mode(0, 5)  # more objects than capacity
     with pytest.raises(_lib.RtError):
         r.upload_header(h)
+    with pytest.raises(_lib.RtError):
+        r.compute_frames(h, 3, 0, 1)
     r.close()
     with pytest.raises(_lib.RtError):
         Renderer(16, 16, 4, 300)  # spp above the supported 256
