@@ -20,7 +20,8 @@
  *   - normalize(v) = v * (1.0f / sqrtf(dot(v,v))), length(v) = sqrtf(dot(v,v)), IEEE / and
  *     sqrtf (the correctly rounded form of the rsqrt-multiply GLSL compilers emit);
  *   - sin() inside random() = rto_sin(): binary32 Cody-Waite reduction by pi/2 (3-part
- *     constant, explicit fmaf) + Cephes sinf/cosf polynomials — a deterministic sin (abs
+ *     constant, explicit fmaf) + Cephes sinf/cosf polynomials, quadrant = int32(k) & 3 with
+ *     the conversion saturating beyond 2^31 (as v_cvt_i32_f32) — a deterministic sin (abs
  *     error ~1e-7 for |x| < 2^20) both sides reproduce bit for bit; random() only needs a
  *     deterministic hash, and GLSL leaves sin's large-argument precision unspecified;
  *   - shadow_ray's `double t` and its dvec3 length run in binary64 (p_compute.glsl:147-163);
