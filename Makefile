@@ -1,6 +1,8 @@
 # Build the MI355X library (HIP, gfx950) and the CPU oracle (test infrastructure).
 #   make            -> real_time_ray_tracer_amd/librtrt.so, oracle/build/librt_oracle.so, build/rt_headless
 #   make lib|oracle|headless|clean
+#   make ablib      -> build/librtrt_ab.so: the same library plus the experimental A/B kernels and
+#                      their RTRT_* environment switches (tools/ab.py: RTRT_LIB=build/librtrt_ab.so)
 HIPCC    ?= /opt/rocm/bin/hipcc
 CC       ?= gcc
 ARCH     ?= gfx950
@@ -32,6 +34,15 @@ $(OBJDIR)/rt_host.o: $(CSRC)/rt_host.cpp include/rt/*.h | $(OBJDIR)
 $(LIB): $(OBJDIR)/rt_kernels.o $(OBJDIR)/rt_shim.o $(OBJDIR)/rt_host.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
+ABLIB := build/librtrt_ab.so
+$(OBJDIR)/ab_%.o: $(CSRC)/%.hip $(CSRC)/*.h include/rt/*.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -DRTRT_AB=1 -x hip -c $< -o $@
+
+$(ABLIB): $(OBJDIR)/ab_rt_kernels.o $(OBJDIR)/ab_rt_shim.o $(OBJDIR)/rt_host.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+ablib: $(ABLIB)
+
 $(ORACLE): oracle/rt_oracle.c oracle/rt_oracle.h include/rt/layout.h
 	@mkdir -p oracle/build
 	$(CC) $(CFLAGS_ORACLE) -shared -o $@ oracle/rt_oracle.c -lm
@@ -45,4 +56,4 @@ $(OBJDIR):
 clean:
 	rm -rf build oracle/build $(LIB)
 
-.PHONY: all lib oracle headless clean
+.PHONY: all lib oracle headless ablib clean

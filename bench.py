@@ -41,8 +41,29 @@ CONFIGS = {
     "c": (1920, 1080, 64, 16, 2, "config (c): 1920x1080, 64 spheres, AO 16 spp (mode 2)"),
     "d": (3840, 2160, 64, 16, 1, "config (d): 3840x2160, 64 spheres, AO 16 spp + temporal/spatial post-process (mode 1)"),
     "e": (7680, 4320, 256, 64, 2, "config (e): 7680x4320, 256 spheres, AO 64 spp (mode 2)"),
+    # scenes with planes (not BASELINE configs: the plane path's own measurement)
+    "p": (3840, 2160, 65, 16, 1, "config (d) + one ground plane (64 spheres + 1 plane = 65 objects), AO 16 spp + "
+                                 "post-process (mode 1)"),
+    "s1": (3840, 2160, 10, 16, 1, "the reference's scene1 (4 spheres + 1 plane, src/scene.h:15-65) at 3840x2160, "
+                                  "AO 16 spp + post-process (mode 1)"),
 }
-CONFIG_INDEX = {"a": 0, "b": 1, "c": 2, "d": 3, "e": 4}
+CONFIG_INDEX = {"a": 0, "b": 1, "c": 2, "d": 3, "e": 4, "p": 3, "s1": 3}
+
+
+def config_header(name: str):
+    """The seeded scene of a config: synthetic spheres (SURVEY §8d, seed 1234 + config index);
+    "p" adds a ground plane y = -2.5 to config (d)'s scene; "s1" is the reference's scene1."""
+    from real_time_ray_tracer_amd import Header, aspect_for
+
+    W, H, S, spp, _, _ = CONFIGS[name]
+    if name == "s1":
+        return Header.builtin(1, spp, aspect_for(W, H), num_shapes=S)
+    if name == "p":
+        h = Header.synthetic(S - 1, spp, 1234 + CONFIG_INDEX[name], aspect_for(W, H), num_shapes=S)
+        h.pack_plane(S - 1, (0.0, 1.0, 0.0), -2.5, (0.45, 0.4, 0.35), reflectivity=1.0)
+        h.set_mode(0, S)
+        return h
+    return Header.synthetic(S, spp, 1234 + CONFIG_INDEX[name], aspect_for(W, H))
 
 FLOP_PER_TEST = 20          # SURVEY §8d: ~20 FLOP per ray-sphere test (FMA = 2 FLOP)
 PEAK_FP32_TFLOPS = 157.3    # MI355X_MICROARCH.md: peak FP32 vector (spec)
@@ -68,7 +89,7 @@ def cpu_baseline(cfg_name: str, target_s: float) -> dict:
 
     W, H, S, spp, mode, _ = CONFIGS[cfg_name]
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    h = Header.synthetic(S, spp, 1234 + CONFIG_INDEX[cfg_name], aspect_for(W, H))
+    h = config_header(cfg_name)
     progs = {1: [oracle.AOP_COMPUTE, oracle.AOP_POSTPROCESSING], 2: [oracle.AO_COMPUTE],
              3: [oracle.P_COMPUTE], 4: [oracle.H_COMPUTE]}[mode]
 
@@ -156,7 +177,8 @@ def main():
     cdev = dev if args.backend == "nccl" else torch.device("cpu")  # collective tensors
 
     W, H, S, spp, mode, desc = CONFIGS[args.config]
-    header = Header.synthetic(S, spp, 1234 + CONFIG_INDEX[args.config], aspect_for(W, H))
+    header = config_header(args.config)
+    nobj = header.num_objects
     # a dedicated stream: the renderer, the gather and torch's copies are all ordered on it
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
@@ -184,7 +206,7 @@ def main():
             t0 = 0.0
             for k in range(frames):
                 header.fill_rand_buffer(7000 + k) if mode in (1, 2) else header.moving_light(False)
-                header.set_mode(f, S)
+                header.set_mode(f, nobj)
                 r.upload_header(header)
                 if timed_wall and k == 8:
                     r.synchronize()
@@ -271,7 +293,7 @@ def main():
             header.fill_rand_buffer(7000 + k)
         else:
             header.moving_light(False)
-        header.set_mode(state["frame"], S)
+        header.set_mode(state["frame"], nobj)
         rend.upload_header(header)
         if gather is not None:
             with torch.cuda.stream(streams["out"]):  # the post-process writes the strip buffer there

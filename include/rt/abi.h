@@ -125,6 +125,12 @@ int rt_compute_frames(rt_ctx* ctx, float* header, int mode, int frame, int n, ui
  * pixels/normals/depth: [F][W][R] vec4 (x-major, y fastest; R = rows of this context),
  * image: [R][W] rgba32f (row 0 = row_begin, bottom-left origin like the GL texture). */
 int rt_download(rt_ctx* ctx, float* pixels, float* normals, float* depth, float* image);
+/* rt_download of the window of columns [x0, x1) x frame rows [y0, y1) (inside this context's
+ * rows): pixels/normals/depth as [F][x1-x0][y1-y0] vec4 (the reference's x-major, y-fastest
+ * order restricted to the window), image as [y1-y0][x1-x0] rgba32f.  Any pointer may be NULL.
+ * For checking regions of large frames without copying the whole ring. */
+int rt_download_rect(rt_ctx* ctx, int x0, int x1, int y0, int y1, float* pixels, float* normals, float* depth,
+                     float* image);
 /* Upload a reference-layout g-buffer ring ([F][W][R] vec4 each; NULL = leave as is). */
 int rt_upload_gbuffer(rt_ctx* ctx, const float* pixels, const float* normals, const float* depth);
 /* Device pointer of the context's image ([R][W] float4), for collectives. */

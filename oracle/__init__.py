@@ -41,6 +41,9 @@ def load():
     fp = C.POINTER(C.c_float)
     lib.rto_run_program.argtypes = [fp, C.POINTER(rto_dims), C.c_int, C.c_int, fp, C.c_int, C.c_int, C.c_int]
     lib.rto_run_program.restype = C.c_int
+    lib.rto_run_program_window.argtypes = [fp, C.POINTER(rto_dims), C.c_int, C.c_int, fp, C.c_int, C.c_int, C.c_int,
+                                           C.c_int, C.c_int]
+    lib.rto_run_program_window.restype = C.c_int
     lib.rto_dispatch.argtypes = [fp, C.POINTER(rto_dims), C.c_int, C.c_int, fp, C.c_int]
     lib.rto_dispatch.restype = C.c_int
     lib.rto_sin.argtypes = [C.c_float]
@@ -67,10 +70,12 @@ def dims(W, H, S, AA, F=8, D=20, gy0=0, gh=None) -> rto_dims:
 
 
 def run_program(ssbo: np.ndarray, d: rto_dims, program: int, frame: int, image=None, y0=None, y1=None,
-                nthreads: int = 0) -> None:
+                nthreads: int = 0, x0: int = 0, x1=None) -> None:
+    """Rows [y0, y1) (default: the g-buffer band) x columns [x0, x1) (default: all)."""
     y0 = d.gy0 if y0 is None else y0
     y1 = d.gy0 + d.gh if y1 is None else y1
-    rc = load().rto_run_program(_fp(ssbo), C.byref(d), program, frame, _fp(image), y0, y1, nthreads)
+    x1 = d.W if x1 is None else x1
+    rc = load().rto_run_program_window(_fp(ssbo), C.byref(d), program, frame, _fp(image), y0, y1, x0, x1, nthreads)
     if rc != 0:
         raise ValueError(f"rto_run_program rejected its arguments (program {program})")
 

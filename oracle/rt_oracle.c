@@ -561,11 +561,12 @@ static void post_main(octx* c, const float* snap /* [W][gh] vec4 */, int x, int 
 /* ------------------------------------------------------------------------------------ */
 /* drivers                                                                               */
 /* ------------------------------------------------------------------------------------ */
-int rto_run_program(float* ssbo, const rto_dims* d, int program, int frame, float* image, int y0,
-                    int y1, int nthreads) {
+int rto_run_program_window(float* ssbo, const rto_dims* d, int program, int frame, float* image, int y0,
+                           int y1, int x0, int x1, int nthreads) {
   octx c;
   if (octx_init(&c, ssbo, d, frame) != 0) return -1;
   if (y0 < d->gy0 || y1 > d->gy0 + d->gh || y0 > y1) return -1;
+  if (x0 < 0 || x1 > d->W || x0 > x1) return -1;
   if (program < RTO_AOP_COMPUTE || program > RTO_H_COMPUTE) return -1;
 #ifdef _OPENMP
   int nt = nthreads > 0 ? nthreads : omp_get_max_threads();
@@ -582,7 +583,7 @@ int rto_run_program(float* ssbo, const rto_dims* d, int program, int frame, floa
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
 #endif
     for (int y = y0; y < y1; y++)
-      for (int x = 0; x < W; x++) post_main(&c, snap, x, y, image);
+      for (int x = x0; x < x1; x++) post_main(&c, snap, x, y, image);
     free(snap);
     return 0;
   }
@@ -590,7 +591,7 @@ int rto_run_program(float* ssbo, const rto_dims* d, int program, int frame, floa
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
 #endif
   for (int y = y0; y < y1; y++) {
-    for (int x = 0; x < W; x++) {
+    for (int x = x0; x < x1; x++) {
       switch (program) {
         case RTO_P_COMPUTE: p_main(&c, x, y, image); break;
         case RTO_H_COMPUTE: h_main(&c, x, y, image); break;
@@ -601,6 +602,11 @@ int rto_run_program(float* ssbo, const rto_dims* d, int program, int frame, floa
     }
   }
   return 0;
+}
+
+int rto_run_program(float* ssbo, const rto_dims* d, int program, int frame, float* image, int y0,
+                    int y1, int nthreads) {
+  return d ? rto_run_program_window(ssbo, d, program, frame, image, y0, y1, 0, d->W, nthreads) : -1;
 }
 
 int rto_dispatch(float* ssbo, const rto_dims* d, int mode, int frame, float* image, int nthreads) {

@@ -58,6 +58,12 @@ enum { RTO_AOP_COMPUTE = 1, RTO_AOP_POSTPROCESSING = 2, RTO_AO_COMPUTE = 3,
 int rto_run_program(float* ssbo, const rto_dims* d, int program, int frame, float* image,
                     int y0, int y1, int nthreads);
 
+/* rto_run_program over the window of columns [x0, x1) only (the g-buffer and image keep their
+ * full width W).  A post-process pixel reads its left/right neighbours' pixels of the same
+ * pass-1 output, so a window checked after the post-process needs pass 1 over [x0-1, x1+1). */
+int rto_run_program_window(float* ssbo, const rto_dims* d, int program, int frame, float* image,
+                           int y0, int y1, int x0, int x1, int nthreads);
+
 /* compute() of src/main.cpp:553-578 for modes 1..4 over the whole g-buffer band; returns the
  * next frame slot. */
 int rto_dispatch(float* ssbo, const rto_dims* d, int mode, int frame, float* image, int nthreads);

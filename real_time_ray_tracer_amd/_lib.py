@@ -54,6 +54,7 @@ SIGNATURES = {
     "rt_dispatch": (C.c_int, [_ctx, C.c_int, C.c_int]),
     "rt_compute_frames": (C.c_int, [_ctx, _fp, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int]),
     "rt_download": (C.c_int, [_ctx, _fp, _fp, _fp, _fp]),
+    "rt_download_rect": (C.c_int, [_ctx, C.c_int, C.c_int, C.c_int, C.c_int, _fp, _fp, _fp, _fp]),
     "rt_upload_gbuffer": (C.c_int, [_ctx, _fp, _fp, _fp]),
     "rt_image_device_ptr": (_vp, [_ctx]),
     "rt_bind_image": (C.c_int, [_ctx, _vp]),

@@ -271,6 +271,20 @@ __device__ __forceinline__ void sphere_candidate(f3 pos, f3 dir, float4 g, int i
   }
 }
 
+// One plane of the min-t scan, tested out of index order (after the spheres): plane_eval_ray
+// (p_compute.glsl:111-119) and the scan's acceptance, with the tie rule made explicit.  The
+// sequential scan (`res > thr && (res < t || t < 0)`, ascending i) ends with the accepted
+// candidate of least t and, among equal t, least index; that lexicographic minimum does not
+// depend on the visiting order, so testing the planes after the spheres gives the same (t, ind).
+// a = (normal, bits(index)), b = (p0, 0) (rt_kernels.h plane table).
+__device__ __forceinline__ void plane_candidate(f3 pos, f3 dir, float4 a, float4 b, float thr, float& t, int& ind) {
+  const float res = plane_eval(pos, dir, a, b);
+  const int i = __float_as_int(a.w);
+  const bool acc = res > thr && (t < 0.0f || res < t || (res == t && i < ind));
+  t = acc ? res : t;
+  ind = acc ? i : ind;
+}
+
 // All-sphere closest hit with the min-t update inside the hit branch and the geometry of 4
 // spheres fetched before any of them is tested (V = 2: global table read with wave-uniform
 // scalar loads; V = 0: closest_hit).  Bit-identical to closest_hit.

@@ -28,6 +28,10 @@ struct FrameParams {
   float Lx, Ly, Lz;          // light_pos
   float4 bg;                 // background
   const float4* shapes;      // compact table [4][S]: geo, geo2, col, aux (rt_device.h)
+  // derived from `shapes` by launch_program (sphere_table / plane_table below):
+  const float4* sph;         // [S] sphere-only geometry: geo for spheres, NaN for every other shape
+  const float4* planes;      // [nplanes][2]: (normal, bits(index)), (p0, 0) of the planes among [0, nobj)
+  int nplanes;               // set by the host (rt_shim) from the header's shape ids
   const float4* rb;          // rand_buffer[2*spp]
   float4* out_pix;           // colour destination [band_rows][W]
   float4* nrm;               // normals_buffer slot `frame` [band_rows][W]
@@ -49,11 +53,23 @@ struct FrameParams {
   unsigned long long* row_counters;
 };
 
+// Device shape table of one header copy, in float4 units from its base (rt_shim fills it):
+//   [0, 4S)          geo, geo2, col, aux        (rt_device.h "scene tables")
+//   [4S, 5S)         sph: geo of spheres, NaN of other shapes (never accepted by sphere_candidate)
+//   [5S, 7S)         planes: 2 float4 per plane, compacted, ascending index
+//   [7S, 7S + 2spp)  rand_buffer
+__host__ __device__ constexpr size_t sphere_table(int S) { return (size_t)4 * S; }
+__host__ __device__ constexpr size_t plane_table(int S) { return (size_t)5 * S; }
+__host__ __device__ constexpr size_t rand_table(int S) { return (size_t)7 * S; }
+__host__ __device__ constexpr size_t table_vec4(int S, int spp) { return (size_t)7 * S + (size_t)2 * spp; }
+
 enum KernelId { K_AOP = 1, K_POST = 2, K_AO = 3, K_PHONG = 4, K_HYBRID = 5 };
 
-// Launch `program` (RT_PROG_* numbering) on `stream`.  all_spheres selects the specialised
-// intersection loop.  Returns hipSuccess or the launch error.
-hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, hipStream_t stream);
+// Launch `program` (RT_PROG_* numbering) on `stream`.  Scenes with planes (p.nplanes > 0)
+// take the plane-testing instantiations; every other shape but spheres and planes is never
+// hit (eval_ray returns -1 for it, p_compute.glsl:121-138) and is skipped through the NaN
+// entries of the sphere table.  Returns hipSuccess or the launch error.
+hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream);
 
 // Device math self-test (rt_selftest_math).
 hipError_t launch_selftest(int fn, const float* d_in, float* d_out, size_t n, hipStream_t stream);

@@ -1,19 +1,25 @@
 // rt_kernels.hip — gfx950 kernels for the per-pixel ray-scene hot path.
 //
-//   phong_kernel   <- resources/p_compute.glsl   (mode 3)
-//   hybrid_kernel  <- resources/h_compute.glsl   (mode 4)
-//   ao_kernel      <- resources/ao_compute.glsl  (mode 2) / aop_compute.glsl (mode 1 pass 1)
-//   post_kernel    <- resources/aop_postprocessing.glsl (mode 1 pass 2)
+//   phong_kernel     <- resources/p_compute.glsl   (mode 3)
+//   hybrid_kernel    <- resources/h_compute.glsl   (mode 4)
+//   ao_batch_kernel  <- resources/ao_compute.glsl  (mode 2) / aop_compute.glsl (mode 1 pass 1)
+//   post_kernel      <- resources/aop_postprocessing.glsl (mode 1 pass 2)
 //
 // The reference dispatches W x H single-lane workgroups (local_size 1x1, p_compute.glsl:26).
-// Here a 256-lane workgroup (4 wave64) owns a tile: one lane per pixel (modes 3/4) or one
-// lane per pixel-sample (modes 1/2).  The scene table (<= a few KB) is staged into LDS once
-// per workgroup and read by wave-uniform broadcast.  AO samples of a pixel are combined in
-// sample order by the pixel's sample-0 lane, so the sum order matches the reference's
-// sequential `result_color += ambient_occlusion(dir, aa)` (ao_compute.glsl:303-330).
+// Here a 256-lane workgroup (4 wave64) owns a 16x16 pixel tile (modes 3/4, one lane per
+// pixel), and a one-wave workgroup owns a pool of 256 pixel-samples (modes 1/2).  The sphere
+// table is read on the scalar path with wave-uniform loads; camera rays are cone-culled per
+// wave / pool.  Planes are tested after the spheres of each segment.  Per-sample AO results are
+// combined in sample order, so the sum order matches the reference's sequential
+// `result_color += ambient_occlusion(dir, aa)` (ao_compute.glsl:303-330).
+//
+// RTRT_AB (make ablib, tools only): the experimental and superseded kernels used by the A/B
+// tools (lane-per-sample AO, streaming AO, LDS-table Phong/hybrid, timing ablations).
 #include <hip/hip_runtime.h>
 
+#if RTRT_AB
 #include <cstdlib>
+#endif
 
 #include "rt_device.h"
 #include "rt_kernels.h"
@@ -273,26 +279,90 @@ __device__ __forceinline__ bool bounce_cone_keep_pt(const ConeB& c, float4 g, fl
   return !(cphi < K);  // (2)
 }
 
+// ---------------------------------------------------------------------------------------
+// Planes (plane_eval_ray, p_compute.glsl:111-119) in the cone-culled kernels.  The spheres
+// keep their culled, ascending scan over the sphere table (P.sph: planes and every other
+// shape are NaN there, never accepted); the planes are tested after it from the compact plane
+// table and merged by plane_candidate's lexicographic (t, index) rule, which is the result of
+// the reference's ascending scan whatever the visiting order.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long uniform_mask(unsigned long long m) {
+  return ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
+         (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
+}
+
+// every plane of the scene
+__device__ __forceinline__ void plane_pass(const FrameParams& P, f3 pos, f3 dir, float thr, float& t, int& ind) {
+  for (int k = 0; k < P.nplanes; ++k) plane_candidate(pos, dir, P.planes[2 * k], P.planes[2 * k + 1], thr, t, ind);
+}
+
+// the planes k < 64 whose bit is set in the wave-uniform mask m, and every plane k >= 64
+__device__ __forceinline__ void plane_pass_masked(const FrameParams& P, unsigned long long m, f3 pos, f3 dir, float thr,
+                                                  float& t, int& ind) {
+  while (m) {
+    const int k = __builtin_ctzll(m);
+    m &= m - 1;
+    plane_candidate(pos, dir, P.planes[2 * k], P.planes[2 * k + 1], thr, t, ind);
+  }
+  for (int k = 64; k < P.nplanes; ++k) plane_candidate(pos, dir, P.planes[2 * k], P.planes[2 * k + 1], thr, t, ind);
+}
+
+// A plane that no camera ray of the cone can accept.  Every such ray starts at the camera, so
+// its numerator dot(n, p0 - cam) is the same float on every lane (computed here by the same
+// operations).  The ray's t = num / denom is accepted only if denom has num's sign and is
+// outside (-0.001, 0.001); the denominators dot(n, d) of the cone's directions lie within
+// |n| [cos(min(phi + theta, pi)), cos(max(phi - theta, 0))], phi = angle(n, axis).  With a
+// 1e-4 |n| slack (the cone's float error is ~1e-6; the lanes' dot error ~3e-7 |n|) a plane
+// outside that window for its sign is missed by every lane (-1 or a value <= 0, never accepted).
+// NaN fails every comparison and keeps the plane.
+__device__ __forceinline__ bool plane_cone_misses(const ConeF& c, float4 a, float4 b, f3 cam) {
+  const f3 n = xyz(a);
+  const float num = dot(n, xyz(b) - cam);
+  if (num == 0.0f) return true;  // res = +-0 (or NaN): never above a threshold >= 0
+  const float n2 = n.x * n.x + n.y * n.y + n.z * n.z;
+  if (n2 == 0.0f) return true;  // denom = 0: the parallel case, -1
+  const float nl = fast_sqrt(n2);
+  const float cphi = (c.ax * n.x + c.ay * n.y + c.az * n.z) * fast_rcp(nl);
+  const float sphi = fast_sqrt(fmaxf(0.0f, 1.0f - cphi * cphi));
+  if (num > 0.0f) {  // accepted only with denom >= 0.001
+    const float cmax = cphi > c.ct ? 1.0f : cphi * c.ct + sphi * c.st;
+    return nl * (cmax + 1e-4f) < 0.001f;
+  }
+  if (num < 0.0f) {  // accepted only with denom <= -0.001
+    const float cmin = cphi < -c.ct ? -1.0f : cphi * c.ct - sphi * c.st;
+    return nl * (cmin - 1e-4f) > -0.001f;
+  }
+  return false;  // NaN
+}
+
+// wave-uniform mask of the planes k < 64 that the cone does not exclude
+__device__ __forceinline__ unsigned long long plane_cone_mask(const FrameParams& P, const ConeF& cone, f3 cam) {
+  const int k = lane_id_here();
+  const bool keep = k < P.nplanes && !plane_cone_misses(cone, P.planes[2 * k], P.planes[2 * k + 1], cam);
+  return uniform_mask(__ballot(keep));
+}
+
 // Closest hit of the camera rays of a pixel rectangle whose cone is `cone`: per 64-sphere
 // word the wave culls the spheres lane-parallel, then tests the survivors in ascending index
-// order, reading them on the scalar path (wave-uniform index).  Same result as closest_hit.
-__device__ __forceinline__ int closest_hit_cone(const float4* __restrict__ geo, int nobj, const ConeF& cone, f3 cam,
-                                                f3 dir, float thr, float& t_out) {
+// order, reading them on the scalar path (wave-uniform index).  PL: then the planes the cone
+// does not exclude.  Same result as closest_hit.  Must be called by every lane of the wave.
+template <bool PL>
+__device__ __forceinline__ int closest_hit_cone(const FrameParams& P, const float4* __restrict__ geo, int nobj,
+                                                const ConeF& cone, f3 cam, f3 dir, float thr, float& t_out) {
   float t = -1.0f;
   int ind = -1;
   const int lane = threadIdx.x & 63;
   for (int w = 0; w < nobj; w += 64) {
     const int i = w + lane;
     const bool keep = i < nobj && !cone_misses_f(cone, geo[i], cam.x, cam.y, cam.z);
-    unsigned long long m = __ballot(keep);
-    m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
-        (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
+    unsigned long long m = uniform_mask(__ballot(keep));
     while (m) {
       const int k = w + __builtin_ctzll(m);
       m &= m - 1;
       sphere_candidate(cam, dir, geo[k], k, thr, t, ind);
     }
   }
+  if (PL) plane_pass_masked(P, plane_cone_mask(P, cone, cam), cam, dir, thr, t, ind);
   t_out = t;
   return ind;
 }
@@ -311,23 +381,31 @@ __device__ __forceinline__ ConeF wave_tile_cone(const FrameParams& P) {
 // rest are tested as shadow_lit does.  "Some occluder exists" does not depend on the order.
 // Must be called by every lane of the wave (ballots and shuffles).
 constexpr int kShadowConeMinObj = 8;
-__device__ __forceinline__ bool shadow_lit_cone(const float4* __restrict__ geo, int n, f3 light, f3 pos, bool need) {
+// the binary64 occluder test of shadow_ray (p_compute.glsl:155-163) for one object's float t
+__device__ __forceinline__ bool shadow_occludes(float tf, f3 l, double dlen) {
+  const double t = (double)tf;
+  if (!(t > (double)0.0001f)) return false;
+  const double dx = t * (double)l.x, dy = t * (double)l.y, dz = t * (double)l.z;
+  return sqrt(fma(dz, dz, fma(dy, dy, dx * dx))) < dlen;
+}
+// PL: planes occlude too (any shape type does, p_compute.glsl:153); they are tested after the
+// spheres ("some occluder exists" does not depend on the order).
+template <bool PL>
+__device__ __forceinline__ bool shadow_lit_cone(const FrameParams& P, const float4* __restrict__ geo, int n, f3 light,
+                                                f3 pos, bool need) {
   const f3 lv = light - pos;
   const f3 l = normalize(lv);
   const float len = sqrtf(dot(lv, lv));
   const f3 np = pos + 0.01f * l;
   const double dlen = (double)len;
   if (__ballot(need) == 0) return true;
+  bool lit = true;
+  if (PL)
+    for (int k = 0; k < P.nplanes; ++k)
+      if (need && lit && shadow_occludes(plane_eval(np, l, P.planes[2 * k], P.planes[2 * k + 1]), l, dlen)) lit = false;
   if (n <= kShadowConeMinObj) {  // small scenes: the cone costs more than it saves
-    bool lit = true;
     for (int k = 0; k < n; ++k) {
-      if (need && lit) {
-        const double t = (double)sphere_eval_shadow(np, l, geo[k]);
-        if (t > (double)0.0001f) {
-          const double dx = t * (double)l.x, dy = t * (double)l.y, dz = t * (double)l.z;
-          if (sqrt(fma(dz, dz, fma(dy, dy, dx * dx))) < dlen) lit = false;
-        }
-      }
+      if (need && lit && shadow_occludes(sphere_eval_shadow(np, l, geo[k]), l, dlen)) lit = false;
     }
     return lit;
   }
@@ -347,7 +425,6 @@ __device__ __forceinline__ bool shadow_lit_cone(const float4* __restrict__ geo, 
   cone.ct = cd;
   cone.st = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - cd * cd));
   const bool wide = !(cd > 0.05f);  // nearly a half-space: test everything
-  bool lit = true;
   const int lane = threadIdx.x & 63;
   for (int w = 0; w < n; w += 64) {
     const int i = w + lane;
@@ -356,19 +433,11 @@ __device__ __forceinline__ bool shadow_lit_cone(const float4* __restrict__ geo, 
       const float4 g = geo[i];
       keep = !cone_misses_f(cone, make_float4(g.x, g.y, g.z, g.w + 1e-4f), light.x, light.y, light.z);
     }
-    unsigned long long m = __ballot(keep);
-    m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
-        (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
+    unsigned long long m = uniform_mask(__ballot(keep));
     while (m) {
       const int k = w + __builtin_ctzll(m);
       m &= m - 1;
-      if (need && lit) {
-        const double t = (double)sphere_eval_shadow(np, l, geo[k]);
-        if (t > (double)0.0001f) {
-          const double dx = t * (double)l.x, dy = t * (double)l.y, dz = t * (double)l.z;
-          if (sqrt(fma(dz, dz, fma(dy, dy, dx * dx))) < dlen) lit = false;
-        }
-      }
+      if (need && lit && shadow_occludes(sphere_eval_shadow(np, l, geo[k]), l, dlen)) lit = false;
     }
   }
   return lit;
@@ -377,18 +446,40 @@ __device__ __forceinline__ bool shadow_lit_cone(const float4* __restrict__ geo, 
 // ---------------------------------------------------------------------------------------
 // mode 3 — p_compute.glsl:168-245
 // ---------------------------------------------------------------------------------------
-template <bool ALLSPH>
+// shadow_ray over the sphere table (every lane on its own; the hybrid kernel's bounces), with
+// the planes first when the scene has some (any order: "some occluder exists")
+template <bool PL>
+__device__ __forceinline__ bool shadow_lit_sph(const FrameParams& P, const float4* __restrict__ geo, int n, f3 light,
+                                               f3 pos) {
+  const f3 lv = light - pos;
+  const f3 l = normalize(lv);
+  const float len = sqrtf(dot(lv, lv));
+  const f3 np = pos + 0.01f * l;
+  const double dlen = (double)len;
+  if (PL)
+    for (int k = 0; k < P.nplanes; ++k)
+      if (shadow_occludes(plane_eval(np, l, P.planes[2 * k], P.planes[2 * k + 1]), l, dlen)) return false;
+  for (int i = 0; i < n; ++i)
+    if (shadow_occludes(sphere_eval_shadow(np, l, geo[i]), l, dlen)) return false;
+  return true;
+}
+
+// The kernels below come in two families.  ALLSPH (production): the sphere table P.sph is
+// read on the scalar path from global memory, the camera rays of each wave's 8x8 tile and
+// their shadow rays are cone-culled, and PL adds the scene's planes (plane table, tested after
+// the spheres).  !ALLSPH (A/B builds only): the whole shape table staged in LDS, every shape
+// tested through eval_ray's id dispatch, no culling.
+template <bool ALLSPH, bool PL = false>
 __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
-  // all-sphere scenes: the table is read on the scalar path from global memory and the
-  // primary rays of each wave's 8x8 tile are cone-culled; general scenes: LDS table
   extern __shared__ float4 lds[];
   if (!ALLSPH) {
     stage_shapes(P, lds);
     __syncthreads();
   }
   const int n = P.nobj;
-  const float4* geo = ALLSPH ? P.shapes : lds;
-  const float4 *geo2 = geo + (ALLSPH ? P.S : n), *col = geo + 2 * (ALLSPH ? P.S : n);
+  const float4* tab = ALLSPH ? P.shapes : lds;  // geo | geo2 | col
+  const float4* geo = ALLSPH ? P.sph : lds;     // what the sphere tests read
+  const float4 *geo2 = tab + (ALLSPH ? P.S : n), *col = tab + 2 * (ALLSPH ? P.S : n);
   int x, y;
   tile_xy(x, y, P.trace_row0);
   const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
@@ -398,14 +489,14 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
   int ind;
   if (ALLSPH) {
     const ConeF cone = wave_tile_cone(P);
-    ind = closest_hit_cone(geo, n, cone, cam, dir, 0.0f, t);
+    ind = closest_hit_cone<PL>(P, geo, n, cone, cam, dir, 0.0f, t);
   } else {
     ind = closest_hit<ALLSPH>(geo, geo2, n, cam, dir, 0.0f, t);
   }
   count_work(P, active, y, 1u, active && ind != -1 ? 1u : 0u);
   const bool need = active && ind != -1;
   bool lit_w = true;
-  if (ALLSPH) lit_w = shadow_lit_cone(geo, n, light, cam + t * dir, need);  // every lane takes part
+  if (ALLSPH) lit_w = shadow_lit_cone<PL>(P, geo, n, light, cam + t * dir, need);  // every lane takes part
   if (!active) return;
   float r, g, b;
   if (ind == -1) {
@@ -413,8 +504,8 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
   } else {
     f3 curr = cam + t * dir;
     bool lit = ALLSPH ? lit_w : shadow_lit<ALLSPH>(geo, geo2, n, light, curr);
-    int id = ALLSPH ? SHAPE_SPHERE : __float_as_int(geo2[ind].w);
-    f3 nn = shape_normal(geo[ind], id, curr);
+    int id = (ALLSPH && !PL) ? SHAPE_SPHERE : __float_as_int(geo2[ind].w);
+    f3 nn = shape_normal(tab[ind], id, curr);
     float4 c = col[ind];
     if (lit) {
       f3 l = normalize(light - curr);
@@ -432,17 +523,18 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
 // ---------------------------------------------------------------------------------------
 // mode 4 — h_compute.glsl:186-321
 // ---------------------------------------------------------------------------------------
-template <bool ALLSPH>
+template <bool ALLSPH, bool PL = false>
 __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
-  extern __shared__ float4 lds[];  // general scenes: LDS table; all-sphere: scalar path (phong_kernel)
+  extern __shared__ float4 lds[];  // !ALLSPH: LDS table (see phong_kernel)
   if (!ALLSPH) {
     stage_shapes(P, lds);
     __syncthreads();
   }
   const int n = P.nobj;
-  const float4* geo = ALLSPH ? P.shapes : lds;
+  const float4* tab = ALLSPH ? P.shapes : lds;
+  const float4* geo = ALLSPH ? P.sph : lds;
   const int stride = ALLSPH ? P.S : n;
-  const float4 *geo2 = geo + stride, *col = geo + 2 * stride, *aux = geo + 3 * stride;
+  const float4 *geo2 = tab + stride, *col = tab + 2 * stride, *aux = tab + 3 * stride;
   int x, y;
   tile_xy(x, y, P.trace_row0);
   const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
@@ -458,8 +550,8 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
   bool lit0 = true;
   if (ALLSPH) {  // the camera rays of the wave's 8x8 tile and their shadow rays, cone-culled
     const ConeF cone = wave_tile_cone(P);
-    ind0 = closest_hit_cone(geo, n, cone, pos, dir, 0.001f, t0);
-    lit0 = shadow_lit_cone(geo, n, light, pos + t0 * dir, active && ind0 != -1);  // every lane takes part
+    ind0 = closest_hit_cone<PL>(P, geo, n, cone, pos, dir, 0.001f, t0);
+    lit0 = shadow_lit_cone<PL>(P, geo, n, light, pos + t0 * dir, active && ind0 != -1);  // every lane takes part
   }
   for (int seg = 0; active && seg < P.D; ++seg) {  // helper depth D, D-1, ..., 1
     // ---- hybrid_helper ----
@@ -470,6 +562,7 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
       ind = ind0;
     } else if (ALLSPH) {
       ind = closest_hit_pf(geo, n, pos, dir, 0.001f, t);
+      if (PL) plane_pass(P, pos, dir, 0.001f, t, ind);
     } else {
       ind = closest_hit<ALLSPH>(geo, geo2, n, pos, dir, 0.001f, t);
     }
@@ -483,9 +576,11 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
     } else {
       float4 att = col[ind];
       f3 curr = pos + t * dir;
-      bool lit = (ALLSPH && seg == 0) ? lit0 : shadow_lit<ALLSPH>(geo, geo2, n, light, curr);
-      int id = ALLSPH ? SHAPE_SPHERE : __float_as_int(geo2[ind].w);
-      f3 nn = shape_normal(geo[ind], id, curr);
+      bool lit = (ALLSPH && seg == 0) ? lit0
+                 : ALLSPH             ? shadow_lit_sph<PL>(P, geo, n, light, curr)
+                                      : shadow_lit<ALLSPH>(geo, geo2, n, light, curr);
+      int id = (ALLSPH && !PL) ? SHAPE_SPHERE : __float_as_int(geo2[ind].w);
+      f3 nn = shape_normal(tab[ind], id, curr);
       if (lit) {
         f3 l = normalize(light - curr);
         float spec = pow500(gclamp(dot(normalize(l - dir), nn), 0.0f, 1.0f));
@@ -529,6 +624,7 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
 // ---------------------------------------------------------------------------------------
 enum { PRIM_HIT = 0, PRIM_MISS = 1, PRIM_EMISSIVE = 2 };
 
+#if RTRT_AB  // the lane-per-sample AO kernel: A/B builds only (the pooled kernel below is production)
 template <bool ALLSPH, int V>
 __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4* __restrict__ gtab) {
   extern __shared__ float4 lds[];
@@ -656,8 +752,10 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4*
   store_color(P, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
 }
 
+#endif  // RTRT_AB
+
 // ---------------------------------------------------------------------------------------
-// Pooled AO (all-sphere scenes).  One wave per workgroup owns a pool of kPool pixel-samples
+// Pooled AO (production, all scenes).  One wave per workgroup owns a pool of kPool pixel-samples
 // (TP = kPool/spp consecutive pixels x spp samples).  New samples are prepared 64 at a time
 // with the whole wave active: primary direction + hemisphere vector + primary hit
 // over the culled set + first-hit shading.  Samples whose path ended at the primary hit are
@@ -685,8 +783,10 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
   return L;
 }
 
+// geo: the sphere table (P.sph).  PL: the scene has planes, tested after the spheres of every
+// segment (plane_candidate) and, for the primary rays, culled against the pool cone.
 template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
-          int SPPC = 0, bool PT = false, bool CNT = true>
+          int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   // CNT = false: the work counters compiled out (timed launches pass none): fewer live scalars
   unsigned long long* const cnts = CNT ? P.counters : nullptr;
@@ -752,14 +852,20 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   const int yl = P.trace_row0 + (int)((p0 + np - 1) / W), xl = (int)((p0 + np - 1) % W);
   int ncull = 0;
   const int nwords = (nobj + 63) >> 6;
+  unsigned long long pmask = 0;  // PL: planes k < 64 the pool's camera rays may hit (wave-uniform)
   {
     const ConeF cone = pool_cone_f(P, yf == yl ? xf : 0, yf == yl ? xl : W - 1, yf, yl);
     for (int w = 0; w < nwords; ++w) {
       int i = (w << 6) + lane;
       bool keep = i < nobj && !cone_misses_f(cone, geo[i], P.cx, P.cy, P.cz);
+      if (PL) keep = keep && geo[i].x == geo[i].x;  // not a plane / other shape (NaN in the sphere table)
       unsigned long long m = __ballot(keep);
       ncull += __popcll(m);
       if (lane == 0) cmask[w] = m;
+    }
+    if (PL) {
+      pmask = plane_cone_mask(P, cone, mk(P.cx, P.cy, P.cz));
+      ncull += __popcll(pmask) + (P.nplanes > 64 ? P.nplanes - 64 : 0);
     }
   }
   __syncthreads();
@@ -847,7 +953,13 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       } else {
         kind = PRIM_HIT;
         f3 curr = cam + t * dr;  // sic: camera origin (ao_compute.glsl:210)
-        f3 nn = normalize(curr - xyz(geo[ind]));
+        f3 nn;
+        if (PL) {  // ao_compute.glsl:211-218: the stored normal of a plane
+          const float4 gi = P.shapes[ind];
+          nn = __float_as_int(P.shapes[P.S + ind].w) == SHAPE_PLANE ? xyz(gi) : normalize(curr - xyz(gi));
+        } else {
+          nn = normalize(curr - xyz(geo[ind]));
+        }
         if (aa == 0 && first) prec[lp] = make_float4(nn.x, nn.y, nn.z, t);
         ps = curr;
         const float reflect = aux[ind].y;
@@ -926,6 +1038,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           }
         }
       }
+      if (PL) plane_pass_masked(P, pmask, bpos, bdir, 0.0001f, t, ind);
       ++nseg;
       if (LAZY && ind != -1 && !(aux[ind].x > 0.9f)) bhemi = hemisphere();
       live = shade(ind, t, bpos, bdir, bhemi, br, bg, bb, D, bitem, true);
@@ -954,6 +1067,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           } else {
             keep = i < nobj && !bounce_cone_misses(cb, geo[i]);
           }
+          if (PL) keep = keep && geo[i].x == geo[i].x;  // planes are tested after the spheres
           unsigned long long m = __ballot(keep);
           m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
               (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
@@ -981,6 +1095,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           }
         }
         if (live) {
+          if (PL) plane_pass(P, bpos, bdir, 0.0001f, t, ind);
           ++nseg;
           live = shade(ind, t, bpos, bdir, bhemi, br, bg, bb, D - 1, bitem, false);
         }
@@ -1066,10 +1181,11 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         t = take ? tb : t;
         ind = take ? ib : ind;
       }
-      const float tt = __shfl(t, rk * G);
-      const int ii = __shfl(ind, rk * G);
+      float tt = __shfl(t, rk * G);
+      int ii = __shfl(ind, rk * G);
       exec_tests += (unsigned long long)((nobj + G - 1) / G);
       if (has) {
+        if (PL) plane_pass(P, pos, dir, 0.0001f, tt, ii);
         ++nseg;
         has = shade(ii, tt, pos, dir, hemi, rr, rg, rb, depth, item, false);
         depth -= 1;
@@ -1082,6 +1198,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     if (has) {
       float t;
       int ind = closest_hit_pf2(geo, nobj, pos, dir, 0.0001f, t);
+      if (PL) plane_pass(P, pos, dir, 0.0001f, t, ind);
       if (ABL == 1) {  // timing ablation: the bounce tests twice
         float z, t2;
         asm volatile("v_mov_b32 %0, 0" : "=v"(z));
@@ -1160,6 +1277,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   }
 }
 
+#if RTRT_AB  // the streaming AO kernel (rejected): A/B builds only
 // ---------------------------------------------------------------------------------------
 // Streaming AO (all-sphere scenes).  The pooled kernel above loses ~25% of its bounce-round
 // lane slots at the end of each pool, when the last long paths run with most lanes idle.
@@ -1525,6 +1643,8 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
   }
 }
 
+#endif  // RTRT_AB
+
 // ---------------------------------------------------------------------------------------
 // mode 1 pass 2 — aop_postprocessing.glsl:57-208, with the documented snapshot semantics:
 // neighbours read `raw` (slot f before filtering); right iff x+1<W, left iff x>0,
@@ -1682,110 +1802,143 @@ size_t shapes_lds_bytes(const FrameParams& p) { return (size_t)4 * p.nobj * size
 
 }  // namespace
 
-// The default pooled AO kernel (variant 7): with split tail rounds and the per-ray first-bounce
-// pre-test when the sphere table fits in LDS (tl), with or without the work counters.
-template <int SPPC>
-void launch_batch7(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStream_t stream, const FrameParams& q) {
+// The production pooled AO kernel: split tail rounds and the per-ray first-bounce pre-test when
+// the sphere table fits in LDS (tl), with or without the work counters (cnt), with or without
+// planes (PL).
+template <int SPPC, bool PL>
+void launch_batch(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStream_t stream, const FrameParams& q) {
   if (tl && cnt)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, true>), g, b, lds, stream, q, q.shapes);
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, true, PL>), g, b, lds, stream, q, q.sph);
   else if (tl)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false>), g, b, lds, stream, q, q.shapes);
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL>), g, b, lds, stream, q, q.sph);
   else if (cnt)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, SPPC, false, true>), g, b, lds, stream, q, q.shapes);
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, SPPC, false, true, PL>), g, b, lds, stream, q, q.sph);
   else
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, SPPC, false, false>), g, b, lds, stream, q, q.shapes);
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, SPPC, false, false, PL>), g, b, lds, stream, q, q.sph);
 }
 
-hipError_t launch_program(int program, const FrameParams& p, bool all_spheres, hipStream_t stream) {
-  if (p.trace_rows <= 0) return hipSuccess;
-  const size_t lds = shapes_lds_bytes(p);
-  if (program == K_AOP || program == K_AO) {
+#if RTRT_AB
+// ---- A/B build only (make ablib -> build/librtrt_ab.so; tools/ab.py, tools/sections.py) -----
+// RTRT_AO_VARIANT selects an experimental AO kernel per launch: 9 (no first-bounce pre-test),
+// 27 (no batched first bounce), 17 (no split tail rounds), 11 (no lazy shortcuts), 20/25 (the
+// streaming sub-pool kernel, 7 / 6 waves), 91-93 (timing ablations: bounce tests twice, culled
+// primary tests twice, section clocks), 0/2 (the lane-per-sample kernel, LDS table / scalar
+// table).  RTRT_GENERAL=1 runs every program on the unculled LDS-table kernels (the pre-plane-
+// support path for scenes with planes).  RTRT_B1_MIN: least live lanes for a batched first bounce.
+static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t stream, long long npix) {
+  const char* ev = getenv("RTRT_AO_VARIANT");
+  const int variant = ev ? atoi(ev) : 7;
+  const char* eb = getenv("RTRT_B1_MIN");
+  q.b1_min = eb ? atoi(eb) : 1;
+  const char* eg = getenv("RTRT_GENERAL");
+  const bool general = (eg && atoi(eg) == 1) || variant == 0 || variant == 2;
+  const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
+  const long long pools = (npix + TP - 1) / TP;
+  const dim3 g((unsigned)pools), b(64);
+  const bool tl = p.nobj <= kTailMaxObj;
+  if (general) {
     const int ppb = kBlock / p.spp >= 1 ? kBlock / p.spp : 1;
     const int block = ppb * p.spp;
-    const long long npix = (long long)p.trace_rows * p.W;
     const long long grid = (npix + ppb - 1) / ppb;
-    const size_t sh = lds + (size_t)block * sizeof(float4);
-    // RTRT_AO_VARIANT: internal A/B switch for kernel experiments (tools/ab.py).
-    // Default 7: the pooled, batch-prepared kernel for all-sphere scenes, with split tail
-    // rounds when the sphere table fits in LDS.  17: without split tail rounds.  11: without the
-    // lazy shortcuts.  20/25: the streaming sub-pool kernel (7 / 6 waves).  91-93: timing
-    // ablations (bounce tests twice, culled primary tests twice, section clocks).  0/2: the
-    // lane-per-sample kernel (the general one, used for scenes with planes).
-    const char* ev = getenv("RTRT_AO_VARIANT");
-    const int variant = ev ? atoi(ev) : 7;
-    const char* eb = getenv("RTRT_B1_MIN");
-    FrameParams q = p;
-    q.b1_min = eb ? atoi(eb) : 1;
-    if (all_spheres && (variant == 7 || variant == 9 || variant == 27 || variant == 17 || variant == 11 || (variant >= 91 && variant <= 93))) {
-      const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
-      const long long pools = (npix + TP - 1) / TP;
-      const size_t psh = (size_t)batch_lds(p.spp, kPool,
-                                           (variant == 7 || variant == 9 || variant == 27 || variant == 93) && p.nobj <= kTailMaxObj
-                                               ? p.nobj : 0).total;
-      const dim3 g((unsigned)pools), b(64);
-      const bool tl = p.nobj <= kTailMaxObj;
-      // timed launches pass no counters: the counter code is compiled out (fewer live scalars)
-      const bool cnt = p.counters || p.row_counters;
-      // spp 4, 16 and 64 (the reference's own scene, configs c/d, config e) have their own
-      // instantiations: constant LDS offsets and it / spp, fewer scalar registers
-      if (variant == 7 && p.spp == 16)
-        launch_batch7<16>(tl, cnt, g, b, psh, stream, q);
-      else if (variant == 7 && p.spp == 64)
-        launch_batch7<64>(tl, cnt, g, b, psh, stream, q);
-      else if (variant == 7 && p.spp == 4)
-        launch_batch7<4>(tl, cnt, g, b, psh, stream, q);
-      else if (variant == 7)
-        launch_batch7<0>(tl, cnt, g, b, psh, stream, q);
-      else if (variant == 9 && p.spp == 16 && tl && !cnt)  // 7 without the per-ray first-bounce pre-test (A/B)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 16, false, false>), g, b, psh, stream, q, p.shapes);
-      else if (variant == 9 && p.spp == 16 && tl)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 16>), g, b, psh, stream, q, p.shapes);
-      else if (variant == 27 && p.nobj <= kTailMaxObj)  // 7 without the batched first bounce (A/B)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true>), g, b, psh, stream, p, p.shapes);
-      else if (variant == 11)
-        hipLaunchKernelGGL((ao_batch_kernel<7, false>), g, b, psh, stream, p, p.shapes);
-      else if (variant == 91)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 1>), g, b, psh, stream, p, p.shapes);
-      else if (variant == 92)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2>), g, b, psh, stream, p, p.shapes);
-      else if (variant == 93 && p.nobj <= kTailMaxObj && p.spp == 16)  // section clocks of variant 7
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true, 16, true>), g, b, psh, stream, q, p.shapes);
-      else if (variant == 93 && p.nobj <= kTailMaxObj)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true>), g, b, psh, stream, q, p.shapes);
-      else if (variant == 93)
-        hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, false, true>), g, b, psh, stream, q, p.shapes);
-      else  // 7 with a large scene, or 17: without the split tail rounds (A/B)
-        hipLaunchKernelGGL(ao_batch_kernel<7>, g, b, psh, stream, p, p.shapes);
-    } else if (all_spheres && (variant == 20 || variant == 25)) {
-      constexpr int kSub = 128, kRing = 2, kWaveSub = 8;  // sub-pool samples, ring slots, sub-pools per wave
-      const int TPs = kSub / p.spp > 0 ? kSub / p.spp : 1;
-      const long long waves = (npix + (long long)kWaveSub * TPs - 1) / ((long long)kWaveSub * TPs);
-      const dim3 g((unsigned)waves), b(64);
-      const size_t sh2 = stream_lds_bytes(p.spp, p.nobj, kSub, kRing, kWaveSub);
-      if (variant == 25)
-        hipLaunchKernelGGL((ao_stream_kernel<6, kSub, kRing>), g, b, sh2, stream, p, p.shapes, kWaveSub, 1.0f / (float)TPs);
-      else
-        hipLaunchKernelGGL((ao_stream_kernel<7, kSub, kRing>), g, b, sh2, stream, p, p.shapes, kWaveSub, 1.0f / (float)TPs);
-    } else if (!all_spheres)
-      hipLaunchKernelGGL((ao_kernel<false, 0>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
-    else if (variant == 2)
-      hipLaunchKernelGGL((ao_kernel<true, 2>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
+    const size_t sh = shapes_lds_bytes(p) + (size_t)block * sizeof(float4);
+    if (variant == 2 && p.nplanes == 0)
+      hipLaunchKernelGGL((ao_kernel<true, 2>), dim3((unsigned)grid), dim3(block), sh, stream, q, q.shapes);
     else
-      hipLaunchKernelGGL((ao_kernel<true, 0>), dim3((unsigned)grid), dim3(block), sh, stream, p, p.shapes);
+      hipLaunchKernelGGL((ao_kernel<false, 0>), dim3((unsigned)grid), dim3(block), sh, stream, q, q.shapes);
+    return true;
+  }
+  if (variant == 7 || p.nplanes > 0) return false;  // production
+  const size_t psh = (size_t)batch_lds(p.spp, kPool, (variant == 9 || variant == 27 || variant == 93) && tl ? p.nobj : 0).total;
+  if (variant == 9 && p.spp == 16 && tl)  // 7 without the per-ray first-bounce pre-test
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 16, false, false>), g, b, psh, stream, q, q.sph);
+  else if (variant == 27 && tl)  // 7 without the batched first bounce
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true>), g, b, psh, stream, q, q.sph);
+  else if (variant == 11)
+    hipLaunchKernelGGL((ao_batch_kernel<7, false>), g, b, psh, stream, q, q.sph);
+  else if (variant == 91)
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 1>), g, b, psh, stream, q, q.sph);
+  else if (variant == 92)
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2>), g, b, psh, stream, q, q.sph);
+  else if (variant == 93 && tl && p.spp == 16)  // section clocks of the production kernel
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true, 16, true>), g, b, psh, stream, q, q.sph);
+  else if (variant == 93 && tl)
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true>), g, b, psh, stream, q, q.sph);
+  else if (variant == 93)
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, false, true>), g, b, psh, stream, q, q.sph);
+  else if (variant == 20 || variant == 25) {
+    constexpr int kSub = 128, kRing = 2, kWaveSub = 8;  // sub-pool samples, ring slots, sub-pools per wave
+    const int TPs = kSub / p.spp > 0 ? kSub / p.spp : 1;
+    const long long waves = (npix + (long long)kWaveSub * TPs - 1) / ((long long)kWaveSub * TPs);
+    const size_t sh2 = stream_lds_bytes(p.spp, p.nobj, kSub, kRing, kWaveSub);
+    if (variant == 25)
+      hipLaunchKernelGGL((ao_stream_kernel<6, kSub, kRing>), dim3((unsigned)waves), b, sh2, stream, q, q.sph, kWaveSub,
+                         1.0f / (float)TPs);
+    else
+      hipLaunchKernelGGL((ao_stream_kernel<7, kSub, kRing>), dim3((unsigned)waves), b, sh2, stream, q, q.sph, kWaveSub,
+                         1.0f / (float)TPs);
+  } else  // 17: without the split tail rounds
+    hipLaunchKernelGGL(ao_batch_kernel<7>, g, b, psh, stream, q, q.sph);
+  return true;
+}
+static bool ab_general() {
+  const char* eg = getenv("RTRT_GENERAL");
+  return eg && atoi(eg) == 1;
+}
+#endif
+
+hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream) {
+  if (p.trace_rows <= 0) return hipSuccess;
+  FrameParams q = p;
+  q.sph = p.shapes + sphere_table(p.S);
+  q.planes = p.shapes + plane_table(p.S);
+  q.b1_min = 1;
+  const bool pl = p.nplanes > 0;
+  if (program == K_AOP || program == K_AO) {
+    const long long npix = (long long)p.trace_rows * p.W;
+#if RTRT_AB
+    if (ab_launch_ao(p, q, stream, npix)) return hipGetLastError();
+#endif
+    const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
+    const long long pools = (npix + TP - 1) / TP;
+    const bool tl = p.nobj <= kTailMaxObj;
+    const size_t psh = (size_t)batch_lds(p.spp, kPool, tl ? p.nobj : 0).total;
+    const dim3 g((unsigned)pools), b(64);
+    // timed launches pass no counters: the counter code is compiled out (fewer live scalars)
+    const bool cnt = p.counters || p.row_counters;
+    // spp 4 (the reference's AA), 16 (configs c/d) and 64 (config e) have their own
+    // instantiations: constant LDS offsets and it / spp, fewer scalar registers
+    if (!pl) {
+      if (p.spp == 16) launch_batch<16, false>(tl, cnt, g, b, psh, stream, q);
+      else if (p.spp == 64) launch_batch<64, false>(tl, cnt, g, b, psh, stream, q);
+      else if (p.spp == 4) launch_batch<4, false>(tl, cnt, g, b, psh, stream, q);
+      else launch_batch<0, false>(tl, cnt, g, b, psh, stream, q);
+    } else {
+      if (p.spp == 16) launch_batch<16, true>(tl, cnt, g, b, psh, stream, q);
+      else if (p.spp == 4) launch_batch<4, true>(tl, cnt, g, b, psh, stream, q);
+      else launch_batch<0, true>(tl, cnt, g, b, psh, stream, q);
+    }
     return hipGetLastError();
   }
   dim3 grid((p.W + 15) / 16, (p.trace_rows + 15) / 16);
+#if RTRT_AB
+  if (ab_general() && (program == K_PHONG || program == K_HYBRID)) {
+    const size_t lds = shapes_lds_bytes(p);
+    if (program == K_PHONG) hipLaunchKernelGGL((phong_kernel<false>), grid, dim3(kBlock), lds, stream, q);
+    else hipLaunchKernelGGL((hybrid_kernel<false>), grid, dim3(kBlock), lds, stream, q);
+    return hipGetLastError();
+  }
+#endif
   switch (program) {
     case K_PHONG:
-      if (all_spheres) hipLaunchKernelGGL(phong_kernel<true>, grid, dim3(kBlock), 0, stream, p);
-      else hipLaunchKernelGGL(phong_kernel<false>, grid, dim3(kBlock), lds, stream, p);
+      if (pl) hipLaunchKernelGGL((phong_kernel<true, true>), grid, dim3(kBlock), 0, stream, q);
+      else hipLaunchKernelGGL((phong_kernel<true, false>), grid, dim3(kBlock), 0, stream, q);
       break;
     case K_HYBRID:
-      if (all_spheres) hipLaunchKernelGGL(hybrid_kernel<true>, grid, dim3(kBlock), 0, stream, p);
-      else hipLaunchKernelGGL(hybrid_kernel<false>, grid, dim3(kBlock), lds, stream, p);
+      if (pl) hipLaunchKernelGGL((hybrid_kernel<true, true>), grid, dim3(kBlock), 0, stream, q);
+      else hipLaunchKernelGGL((hybrid_kernel<true, false>), grid, dim3(kBlock), 0, stream, q);
       break;
     case K_POST:
-      hipLaunchKernelGGL(post_kernel, grid, dim3(kBlock), 0, stream, p);
+      hipLaunchKernelGGL(post_kernel, grid, dim3(kBlock), 0, stream, q);
       break;
     default:
       return hipErrorInvalidValue;

@@ -26,6 +26,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <new>
 #include <utility>
 #include <vector>
@@ -62,8 +63,8 @@ struct rt_ctx {
   int band0 = 0, band_rows = 0;  // strip + 1-row halo (post-process neighbours)
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  float4* d_shapes_buf[kAoStreams] = {};  // [4][S] table + [2*spp] rand_buffer, one copy per AO stream
-  float4* d_rb_buf[kAoStreams] = {};      // = d_shapes_buf[k] + 4*S (one allocation, one upload)
+  float4* d_shapes_buf[kAoStreams] = {};  // shape tables + rand_buffer (rt::table_vec4), one copy per AO stream
+  float4* d_rb_buf[kAoStreams] = {};      // = d_shapes_buf[k] + rt::rand_table(S) (one allocation, one upload)
   float4* d_shapes = nullptr;  // the copy the next dispatch reads
   float4* d_rb = nullptr;
   std::vector<float4*> pix;    // F+pipe_depth buffers
@@ -85,9 +86,9 @@ struct rt_ctx {
   float4* d_image_own = nullptr;
   float4* d_image = nullptr;
   std::vector<float> header;   // host copy of the SSBO prefix
-  std::vector<float4> table;   // host compact shape table
+  std::vector<float4> table;   // host copy of the device table (rt::table_vec4 float4)
   bool have_header = false;
-  bool all_spheres = true;
+  int nplanes = 0;             // planes among simple_shapes[0, nobj)
   int nobj = 0;
   Stage stage[kStageSlots];
   int stage_next = 0;
@@ -118,6 +119,8 @@ int hip_fail(rt_ctx* c, hipError_t e) {
   } while (0)
 
 size_t slot_elems(const rt_ctx* c) { return (size_t)c->band_rows * c->cfg.width; }
+// stride of the device shape tables (>= 1, so an empty scene still has valid pointers)
+int table_stride(const rt_ctx* c) { return std::max(1, c->cfg.num_shapes); }
 
 hipEvent_t get_event(rt_ctx* c) {
   if (!c->event_pool.empty()) {
@@ -227,7 +230,8 @@ void fill_params(const rt_ctx* c, int frame, rt::FrameParams& p) {
   p.img_row0 = c->own0;
   p.img_rows = c->own_rows;
   p.nobj = c->nobj;
-  p.S = c->cfg.num_shapes;
+  p.S = table_stride(c);
+  p.nplanes = c->nplanes;
   p.spp = c->cfg.spp;
   p.inv_spp = 1.0f / (float)c->cfg.spp;
   p.fW = (float)c->cfg.width;
@@ -270,7 +274,7 @@ int launch(rt_ctx* c, int program, const rt::FrameParams& p, hipStream_t st) {
     if (!e0 || !e1) return RT_E_HIP;
     RT_HIP(c, hipEventRecord(e0, st));
   }
-  hipError_t e = rt::launch_program(program, p, c->all_spheres, st);
+  hipError_t e = rt::launch_program(program, p, st);
   if (e != hipSuccess) return hip_fail(c, e);
   if (c->timing) {
     RT_HIP(c, hipEventRecord(e1, st));
@@ -448,9 +452,10 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
   if (!x) return RT_E_NOMEM;
   x->device = device;
   x->cfg = c;
-  // pipelining shape (A/B knobs): RTRT_PIPE_DEPTH in [2, kPipe], RTRT_AO_STREAMS in [1, kAoStreams]
+#if RTRT_AB  // pipelining shape (A/B builds only): RTRT_PIPE_DEPTH in [2, kPipe], RTRT_AO_STREAMS in [1, kAoStreams]
   if (const char* ev = getenv("RTRT_PIPE_DEPTH")) x->pipe_depth = std::min(kPipe, std::max(2, atoi(ev)));
   if (const char* ev = getenv("RTRT_AO_STREAMS")) x->n_ao_streams = std::min(kAoStreams, std::max(1, atoi(ev)));
+#endif
   x->own0 = c.row_begin;
   x->own_rows = c.row_end - c.row_begin;
   x->band0 = std::max(0, c.row_begin - 1);
@@ -484,10 +489,10 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
   }
   if (e == hipSuccess) e = hipMalloc(&x->d_image_own, (size_t)x->own_rows * c.width * sizeof(float4));
   if (e == hipSuccess) e = hipMemsetAsync(x->d_image_own, 0, (size_t)x->own_rows * c.width * sizeof(float4), x->stream);
+  const int Sc = table_stride(x);
   for (int k = 0; k < kAoStreams; ++k) {
-    if (e == hipSuccess)
-      e = hipMalloc(&x->d_shapes_buf[k], ((size_t)4 * std::max(1, c.num_shapes) + (size_t)2 * c.spp) * sizeof(float4));
-    if (e == hipSuccess) x->d_rb_buf[k] = x->d_shapes_buf[k] + (size_t)4 * std::max(1, c.num_shapes);
+    if (e == hipSuccess) e = hipMalloc(&x->d_shapes_buf[k], rt::table_vec4(Sc, c.spp) * sizeof(float4));
+    if (e == hipSuccess) x->d_rb_buf[k] = x->d_shapes_buf[k] + rt::rand_table(Sc);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(x->stream);
   if (e != hipSuccess) {
@@ -510,7 +515,7 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
   x->d_rb = x->d_rb_buf[0];
   x->out_stream = x->own_stream;
   x->header.assign(rt_header_bytes(c.num_shapes, c.spp) / 4, 0.0f);
-  x->table.assign((size_t)4 * std::max(1, c.num_shapes) + (size_t)2 * c.spp, make_float4(0, 0, 0, 0));
+  x->table.assign(rt::table_vec4(Sc, c.spp), make_float4(0, 0, 0, 0));
   *out = x;
   return RT_OK;
 }
@@ -597,7 +602,11 @@ int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
   int nobj = (int)mz;
   std::memcpy(c->header.data(), header, bytes);
   const float* sh = h + rt_off_shapes() / 4;
-  bool allsph = true;
+  const int Sc = table_stride(c);
+  const float qnan = std::numeric_limits<float>::quiet_NaN();
+  float4* sph = c->table.data() + rt::sphere_table(Sc);
+  float4* pln = c->table.data() + rt::plane_table(Sc);
+  int np = 0;
   for (int i = 0; i < S; ++i) {
     const float* s = sh + (size_t)i * 20;
     float idf = s[16 + 3];
@@ -605,10 +614,19 @@ int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
     c->table[i] = make_float4(s[0], s[1], s[2], s[3]);
     float4 g2 = make_float4(s[12], s[13], s[14], 0.0f);
     std::memcpy(&g2.w, &id, 4);
-    c->table[(size_t)S + i] = g2;
-    c->table[(size_t)2 * S + i] = make_float4(s[16], s[17], s[18], s[19]);
-    c->table[(size_t)3 * S + i] = make_float4(s[4 + 3], s[12 + 3], 0.0f, 0.0f);
-    if (i < nobj && id != RT_SHAPE_SPHERE) allsph = false;
+    c->table[(size_t)Sc + i] = g2;
+    c->table[(size_t)2 * Sc + i] = make_float4(s[16], s[17], s[18], s[19]);
+    c->table[(size_t)3 * Sc + i] = make_float4(s[4 + 3], s[12 + 3], 0.0f, 0.0f);
+    // sphere table: the spheres' geometry; every other shape NaN (a NaN discriminant is never
+    // accepted: eval_ray's -1 for shapes it does not intersect, p_compute.glsl:121-138)
+    sph[i] = id == RT_SHAPE_SPHERE ? c->table[i] : make_float4(qnan, qnan, qnan, qnan);
+    if (i < nobj && id == RT_SHAPE_PLANE) {  // plane table: (normal, bits(index)), (p0, 0)
+      float4 a = make_float4(s[0], s[1], s[2], 0.0f);
+      std::memcpy(&a.w, &i, 4);
+      pln[2 * np] = a;
+      pln[2 * np + 1] = make_float4(s[12], s[13], s[14], 0.0f);
+      ++np;
+    }
   }
   RT_HIP(c, hipSetDevice(c->device));
   // pipelined: into the header copy of the next frame, on its AO stream (ordered after the AO
@@ -619,13 +637,13 @@ int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
     if (sr != RT_OK) return sr;
   }
   // table + rand_buffer in one upload (per-frame host cost matters for small strips/frames)
-  std::memcpy(c->table.data() + (size_t)4 * std::max(1, S), h + rt_off_rand(S) / 4, (size_t)2 * spp * sizeof(float4));
+  std::memcpy(c->table.data() + rt::rand_table(Sc), h + rt_off_rand(S) / 4, (size_t)2 * spp * sizeof(float4));
   int rc = staged_copy(c, c->d_shapes_buf[hc], c->table.data(), c->table.size() * sizeof(float4), ao_stream(c));
   if (rc != RT_OK) return rc;
   c->d_shapes = c->d_shapes_buf[hc];
   c->d_rb = c->d_rb_buf[hc];
   c->nobj = nobj;
-  c->all_spheres = allsph;
+  c->nplanes = np;
   c->have_header = true;
   return RT_OK;
 }
@@ -633,14 +651,14 @@ int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
 int rt_upload_rand_buffer(rt_ctx* c, const float* rb, size_t n_vec4) {
   if (!c || !rb || n_vec4 != (size_t)2 * c->cfg.spp) return RT_E_INVAL;
   std::memcpy(c->header.data() + rt_off_rand(c->cfg.num_shapes) / 4, rb, n_vec4 * 16);
-  std::memcpy(c->table.data() + (size_t)4 * std::max(1, c->cfg.num_shapes), rb, n_vec4 * 16);
+  std::memcpy(c->table.data() + rt::rand_table(table_stride(c)), rb, n_vec4 * 16);
   RT_HIP(c, hipSetDevice(c->device));
   const int hc = hdr_copy(c);
   int rc = staged_copy(c, c->d_rb_buf[hc], rb, n_vec4 * 16, ao_stream(c));
   if (rc != RT_OK) return rc;
   // the other copy keeps the shape table: bring it along when switching copies
   if (c->d_shapes != c->d_shapes_buf[hc])
-    RT_HIP(c, hipMemcpyAsync(c->d_shapes_buf[hc], c->d_shapes, (size_t)4 * std::max(1, c->cfg.num_shapes) * sizeof(float4),
+    RT_HIP(c, hipMemcpyAsync(c->d_shapes_buf[hc], c->d_shapes, rt::rand_table(table_stride(c)) * sizeof(float4),
                              hipMemcpyDeviceToDevice, ao_stream(c)));
   c->d_shapes = c->d_shapes_buf[hc];
   c->d_rb = c->d_rb_buf[hc];
@@ -720,6 +738,39 @@ int rt_download(rt_ctx* c, float* pixels, float* normals, float* depth, float* i
   }
   if (image)
     RT_HIP(c, hipMemcpy(image, c->d_image, (size_t)c->own_rows * c->cfg.width * 16, hipMemcpyDeviceToHost));
+  return RT_OK;
+}
+
+int rt_download_rect(rt_ctx* c, int x0, int x1, int y0, int y1, float* pixels, float* normals, float* depth,
+                     float* image) {
+  if (!c) return RT_E_INVAL;
+  const int W = c->cfg.width;
+  if (x0 < 0 || x1 > W || x0 >= x1 || y0 < c->own0 || y1 > c->own0 + c->own_rows || y0 >= y1) return RT_E_INVAL;
+  RT_HIP(c, hipSetDevice(c->device));
+  int rc = join(c);
+  if (rc == RT_OK) rc = sync_all(c);
+  if (rc != RT_OK) return rc;
+  const int w = x1 - x0, h = y1 - y0, F = c->cfg.num_frames;
+  const size_t pitch = (size_t)W * sizeof(float4), row = (size_t)w * sizeof(float4);
+  std::vector<float4> tmp((size_t)w * h);
+  auto rect = [&](const float4* base, int r0) {  // rows [r0, r0 + h) of a [rows][W] device array
+    return hipMemcpy2D(tmp.data(), row, base + (size_t)r0 * W + x0, pitch, row, h, hipMemcpyDeviceToHost);
+  };
+  for (int f = 0; f < F; ++f) {
+    struct { float* dst; const float4* src; } items[3] = {
+        {pixels, c->pix[c->pix_slot[f]]}, {normals, c->nrm[c->nrm_slot[f]]}, {depth, c->dep[c->dep_slot[f]]}};
+    for (auto& it : items) {
+      if (!it.dst) continue;
+      RT_HIP(c, rect(it.src, y0 - c->band0));
+      float* out = it.dst + (size_t)f * w * h * 4;  // [w][h] vec4, y fastest (reference layout)
+      for (int x = 0; x < w; ++x)
+        for (int r = 0; r < h; ++r) std::memcpy(out + ((size_t)x * h + r) * 4, &tmp[(size_t)r * w + x], 16);
+    }
+  }
+  if (image) {
+    RT_HIP(c, rect(c->d_image, y0 - c->own0));
+    std::memcpy(image, tmp.data(), tmp.size() * sizeof(float4));
+  }
   return RT_OK;
 }
 

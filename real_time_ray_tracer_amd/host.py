@@ -256,6 +256,18 @@ class Renderer:
         self._c(self._lib.rt_download(self.ctx, fptr(p), fptr(n), fptr(d), fptr(im)), "rt_download")
         return GBuffer(p, n, d, im)
 
+    def download_rect(self, x0: int, x1: int, y0: int, y1: int, pixels=True, normals=True, depth=True,
+                      image=True) -> GBuffer:
+        """The window [x0, x1) x frame rows [y0, y1): g-buffer [F][w][h][4], image [h][w][4]."""
+        shp = (self.F, x1 - x0, y1 - y0, 4)
+        p = np.empty(shp, np.float32) if pixels else None
+        n = np.empty(shp, np.float32) if normals else None
+        d = np.empty(shp, np.float32) if depth else None
+        im = np.empty((y1 - y0, x1 - x0, 4), np.float32) if image else None
+        self._c(self._lib.rt_download_rect(self.ctx, x0, x1, y0, y1, fptr(p), fptr(n), fptr(d), fptr(im)),
+                "rt_download_rect")
+        return GBuffer(p, n, d, im)
+
     def image(self) -> np.ndarray:
         return self.download(False, False, False, True).image
 

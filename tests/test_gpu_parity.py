@@ -20,8 +20,32 @@ def make_header(scene: str, W: int, H: int, spp: int) -> Header:
     a = aspect_for(W, H)
     if scene.startswith("s") and scene[1:].isdigit():
         return Header.builtin(int(scene[1:]), spp, a)
+    if scene.startswith("syn") and scene.endswith("p"):  # synthetic spheres + one ground plane
+        n = int(scene[3:-1])
+        h = Header.synthetic(n, spp, 1234, a, num_shapes=n + 1)
+        h.pack_plane(n, (0, 1, 0), -2.5, (0.45, 0.4, 0.35))
+        h.set_mode(0, n + 1)
+        return h
     if scene.startswith("syn"):
         return Header.synthetic(int(scene[3:]), spp, 1234, a)
+    if scene == "planetie":  # scene1 + an identical copy of its plane: the lower index must win every tie
+        h = Header.builtin(1, spp, a)
+        h.pack_plane(5, (0, 1, 0), -4.0, (0.9, 0.9, 0.1))
+        h.pack_sphere(6, (0, -0.5, 0), 2.0, (0.1, 0.9, 0.9), reflectivity=0.5)  # copy of sphere 0
+        h.set_mode(0, 7)
+        return h
+    if scene == "manyplanes":  # 20 spheres + 70 planes (> 64: the unmasked plane tail), tilted,
+        rng = np.random.default_rng(7)  # some with non-unit normals, some facing the camera
+        h = Header.synthetic(20, spp, 1234, a, num_shapes=90)
+        for k in range(70):
+            n = rng.normal(size=3)
+            n /= np.linalg.norm(n)
+            if k % 7 == 0:
+                n *= 2.0
+            h.pack_plane(20 + k, n, -float(rng.uniform(25.0, 60.0)), rng.uniform(0.1, 0.9, 3),
+                         reflectivity=float(rng.choice([1.0, 0.3])), emissive=bool(k % 11 == 0))
+        h.set_mode(0, 90)
+        return h
     if scene == "planes":  # spheres + planes + a (never hit) rectangle
         h = Header.builtin(1, spp, a)
         h.pack_plane(5, (1, 0, 0.2), -9.0, (0.2, 0.7, 0.3), reflectivity=0.3)
@@ -61,7 +85,7 @@ def run_both(h: Header, W: int, H: int, mode: int, frames: int, max_depth: int =
 
 
 @pytest.mark.parametrize("mode", [1, 2, 3, 4])
-@pytest.mark.parametrize("scene", ["s1", "s5", "s6", "syn16", "planes", "empty"])
+@pytest.mark.parametrize("scene", ["s1", "s5", "s6", "syn16", "planes", "empty", "planetie", "manyplanes", "syn30p"])
 def test_mode_parity_small(scene, mode):
     W, H, spp = 64, 48, 4
     h = make_header(scene, W, H, spp)
@@ -99,20 +123,22 @@ def test_compute_frames_equals_frame_by_frame(mode):
         assert_bitwise(getattr(g1, name), getattr(g0, name), f"mode {mode} {name}")
 
 
-@pytest.mark.parametrize("spp", [1, 3, 16, 64])
-def test_ao_spp_variants(spp):
+@pytest.mark.parametrize("scene", ["syn16", "syn16p"])
+@pytest.mark.parametrize("spp", [1, 3, 4, 16, 64])
+def test_ao_spp_variants(spp, scene):
     W, H = 40, 24
-    h = make_header("syn16", W, H, spp)
+    h = make_header(scene, W, H, spp)
     g, s, img = run_both(h, W, H, 1, 2)
     assert_close(g.image, img, f"spp {spp} image")
     assert_bitwise(g.depth, s.depth, f"spp {spp} depth")
     assert_bitwise(g.normals, s.normals, f"spp {spp} normals")
 
 
-@pytest.mark.parametrize("nobj", [64, 100, 128, 129, 200])
+@pytest.mark.parametrize("nobj", ["64", "100", "128", "129", "200", "63p", "127p", "150p"])
 def test_ao_scene_sizes(nobj):
-    """Sphere counts around the kernel's 64-sphere words and the 128-sphere LDS table limit
-    (split tail rounds + the first bounce's per-ray pre-test table up to 128, without above)."""
+    """Sphere counts around the kernel's 64-sphere words and the 128-object LDS table limit
+    (split tail rounds + the first bounce's per-ray pre-test table up to 128, without above);
+    "p": plus a ground plane (the plane-testing instantiations, with and without the LDS table)."""
     W, H = 48, 32
     h = make_header(f"syn{nobj}", W, H, 16)
     for mode in (1, 2):

@@ -127,3 +127,38 @@ def test_c_oracle_matches_numpy_restatement(scene, mode):
     # everything but pow() outputs is computed identically
     assert np.array_equal(sn.depth.view(np.uint32), sc.depth.view(np.uint32))
     assert np.array_equal(sn.normals.view(np.uint32), sc.normals.view(np.uint32))
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+def test_oracle_window_equals_whole_frame(mode):
+    """rto_run_program_window (the full-size tile checker): a window's trace passes over the window
+    plus a 1-pixel halo and its post-process over the window give the whole-frame run's values
+    inside the window, over a multi-frame sequence (temporal ring included)."""
+    W, H, spp, frames = 40, 30, 4, 4
+    x0, x1, y0, y1 = 9, 27, 6, 19
+    h0 = Header.builtin(1, spp, aspect_for(W, H))
+    progs = {1: [oracle.AOP_COMPUTE, oracle.AOP_POSTPROCESSING], 2: [oracle.AO_COMPUTE], 3: [oracle.P_COMPUTE],
+             4: [oracle.H_COMPUTE]}[mode]
+    outs = []
+    for window in (False, True):
+        h = h0.copy()
+        d = oracle.dims(W, H, h.S, h.AA)
+        buf = np.zeros(h.data.size + 3 * 8 * W * H * 4, np.float32)
+        img = np.zeros((H, W, 4), np.float32)
+        f = 0
+        for k in range(frames):
+            h.fill_rand_buffer(7000 + k) if mode in (1, 2) else h.moving_light(True)
+            h.set_mode(f, h.num_objects)
+            buf[:h.data.size] = h.data
+            for p in progs:
+                if not window:
+                    oracle.run_program(buf, d, p, f, img)
+                elif p in (oracle.AOP_COMPUTE, oracle.AO_COMPUTE):
+                    oracle.run_program(buf, d, p, f, img, y0 - 1, y1 + 1, x0=x0 - 1, x1=x1 + 1)
+                else:
+                    oracle.run_program(buf, d, p, f, img, y0, y1, x0=x0, x1=x1)
+            f = (f + 1) % 8
+        ring = buf[h.data.size:].reshape(3, 8, W, H, 4)[:, :, x0:x1, y0:y1]
+        outs.append((img[y0:y1, x0:x1].copy(), ring.copy()))
+    np.testing.assert_array_equal(outs[1][0].view(np.uint32), outs[0][0].view(np.uint32))
+    np.testing.assert_array_equal(outs[1][1].view(np.uint32), outs[0][1].view(np.uint32))
