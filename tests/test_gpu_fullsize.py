@@ -114,9 +114,14 @@ def check_window(r: Renderer, cfg: str, frames: int, x0: int, x1: int, y0: int, 
         assert_bitwise(g.depth[:nf], wd[:nf], f"{what} depth")
 
 
-def whole_frame_properties(img: np.ndarray, what: str):
-    assert np.isfinite(img).all(), what
-    assert (img[..., :3] >= 0).all() and (img[..., 3] == 0).all(), what
+def whole_frame_properties(img: np.ndarray, what: str) -> list:
+    """Pixels (x, y) breaking "finite, non-negative, alpha 0"; the caller checks them against the
+    oracle (the reference's own arithmetic can produce NaN, e.g. normalize(vec2(0)) in the
+    jitter, ao_compute.glsl:310-323)."""
+    with np.errstate(invalid="ignore"):
+        bad = ~np.isfinite(img).all(-1) | (img[..., :3] < 0).any(-1) | (img[..., 3] != 0)
+    ys, xs = np.nonzero(bad)
+    return [(int(x), int(y)) for x, y in zip(xs[:4], ys[:4])]
 
 
 @pytest.mark.parametrize("cfg,frames,pipelined", [
@@ -130,8 +135,11 @@ def whole_frame_properties(img: np.ndarray, what: str):
 def test_full_size_tiles(cfg, frames, pipelined):
     r = gpu_render(cfg, frames, pipelined)
     img = r.image()
-    whole_frame_properties(img, cfg)
+    odd = whole_frame_properties(img, cfg)
     tiles = pick_tiles(img)
+    W, H = CONFIGS[cfg][:2]
+    for i, (x, y) in enumerate(odd):  # any non-finite / negative pixel is checked against the oracle
+        tiles[f"odd{i}"] = (min(max(0, x - T // 2), W - T), min(max(0, y - T // 2), H - T))
     for name, (x0, y0) in tiles.items():
         check_window(r, cfg, frames, x0, x0 + T, y0, y0 + T, f"config {cfg} tile {name} at ({x0}, {y0})")
     r.close()
@@ -150,6 +158,6 @@ def test_config_a_whole_frame():
     moving (moving_light, src/main.cpp:541-551)."""
     r = gpu_render("a", 3)
     W, H = CONFIGS["a"][:2]
-    whole_frame_properties(r.image(), "a")
+    assert not whole_frame_properties(r.image(), "a")
     check_window(r, "a", 3, 0, W, 0, H, "config (a) whole frame")
     r.close()
