@@ -31,15 +31,18 @@ $(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/*.h include/rt/*.h | $(OBJDIR)
 $(OBJDIR)/rt_host.o: $(CSRC)/rt_host.cpp include/rt/*.h | $(OBJDIR)
 	$(HIPCC) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude -c $< -o $@
 
-$(LIB): $(OBJDIR)/rt_kernels.o $(OBJDIR)/rt_shim.o $(OBJDIR)/rt_host.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+$(OBJDIR)/rt_group.o: $(CSRC)/rt_group.cpp include/rt/*.h | $(OBJDIR)
+	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Iinclude -c $< -o $@
+
+$(LIB): $(OBJDIR)/rt_kernels.o $(OBJDIR)/rt_shim.o $(OBJDIR)/rt_host.o $(OBJDIR)/rt_group.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 ABLIB := build/librtrt_ab.so
 $(OBJDIR)/ab_%.o: $(CSRC)/%.hip $(CSRC)/*.h include/rt/*.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -DRTRT_AB=1 -x hip -c $< -o $@
 
-$(ABLIB): $(OBJDIR)/ab_rt_kernels.o $(OBJDIR)/ab_rt_shim.o $(OBJDIR)/rt_host.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+$(ABLIB): $(OBJDIR)/ab_rt_kernels.o $(OBJDIR)/ab_rt_shim.o $(OBJDIR)/rt_host.o $(OBJDIR)/rt_group.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 ablib: $(ABLIB)
 

@@ -148,6 +148,56 @@ int rt_compute_one_shader(rt_ctx* ctx, void* ssbo, int frame_num, int program, f
 int rt_compute_two_shaders(rt_ctx* ctx, void* ssbo, int frame_num, int program1, int program2,
                            float* image);
 
+/* ---- multi-device row strips (one process, n strip contexts) ------------------------ */
+/* The reference renders one frame with one glDispatchCompute(WIDTH, HEIGHT, 1)
+ * (src/main.cpp:604, 645-653) and blits the whole image (783-797).  A group splits that frame
+ * into n contiguous row strips, strip i = rows [bounds[i], bounds[i+1]) on device devices[i]
+ * (devices may repeat: several strips on one GPU), each an rt_ctx with its own g-buffer ring
+ * (+ 1-row halo, so strips never exchange data), and assembles the image strips into one
+ * [H][W] rgba32f frame on devices[0]: root-device strips render into their frame rows, the
+ * others copy their strip over xGMI (peer access) on their output stream.  One host thread per
+ * strip enqueues its work.  Results equal a whole-frame rt_ctx bit for bit. */
+typedef struct rt_group rt_group;
+/* cfg: the whole frame (row_begin/row_end ignored); bounds: n+1 increasing rows from 0 to H,
+ * or NULL for equal strips. */
+int rt_group_create(int n, const int* devices, const rt_config* cfg, const int* bounds, rt_group** out);
+int rt_group_destroy(rt_group* g);
+int rt_group_size(rt_group* g);
+int rt_group_bounds(rt_group* g, int* bounds);          /* n+1 entries */
+/* Re-plan the strips (the contexts are re-created: fresh rings, pipelining kept). */
+int rt_group_set_bounds(rt_group* g, const int* bounds);
+/* Strip i's context (kernel stats, counters, downloads of its rows); owned by the group. */
+rt_ctx* rt_group_strip(rt_group* g, int i);
+int rt_group_last_hip_error(rt_group* g);
+/* rt_enable_pipelining on every strip (each on a stream of its own). */
+int rt_group_enable_pipelining(rt_group* g, int on);
+/* Assemble frames into a caller-owned device buffer of H*W float4 on devices[0] (NULL: the
+ * group's own).  Waits for the frames in flight first. */
+int rt_group_bind_frame(rt_group* g, void* device_ptr);
+void* rt_group_frame_device_ptr(rt_group* g);
+/* rt_upload_header for every strip (validated now, uploaded by the next dispatch). */
+int rt_group_upload_header(rt_group* g, const void* header, size_t bytes);
+/* compute() (src/main.cpp:553-578) on every strip + the strip copies; returns the next slot. */
+int rt_group_dispatch(rt_group* g, int mode, int frame);
+/* rt_compute_frames on every strip in parallel (the render loop's host updates per strip,
+ * identical on all), each frame followed by the strip copies.  Returns the next slot. */
+int rt_group_compute_frames(rt_group* g, float* header, int mode, int frame, int n, uint64_t rand_seed,
+                            int light_movement);
+int rt_group_synchronize(rt_group* g);
+/* The assembled frame, [H][W] rgba32f (row 0 = bottom row, like the GL texture). */
+int rt_group_download_image(rt_group* g, float* image);
+/* Cost-balance the strips for `header`/`mode`: one probe frame with per-row work counters
+ * gives the frame's cost profile, rt_plan_strips splits it; then `rounds` plans are timed
+ * strip by strip (wall clock of 16 frames after 8, copy included) with rt_calibrate_row_cost
+ * re-planning between them, and the best is kept (contexts re-created, rings fresh).
+ * strip_ms (n entries, may be NULL): the kept plan's measured ms per frame per strip. */
+int rt_group_balance(rt_group* g, const float* header, int mode, int rounds, double* strip_ms);
+/* Host-only strip planner (no GPU): contiguous strips of nearly equal total row_cost
+ * (row_cost[y] >= 0 for y < H); bounds gets n+1 entries, each strip >= 1 row. */
+int rt_plan_strips(const double* row_cost, int H, int n, int* bounds);
+/* Rescale row_cost so every strip's total equals its measured time (row shape kept). */
+int rt_calibrate_row_cost(double* row_cost, int H, const int* bounds, int n, const double* strip_ms);
+
 /* ---- instrumentation --------------------------------------------------------------- */
 /* When on, every kernel launch is bracketed by HIP events on the context stream. */
 int rt_enable_timing(rt_ctx* ctx, int on);

@@ -36,6 +36,7 @@ class rt_config(C.Structure):
 _fp = C.POINTER(C.c_float)
 _vp = C.c_void_p
 _ctx = C.c_void_p
+_grp = C.c_void_p
 
 # name -> (restype, argtypes); every function declared in include/rt/abi.h
 SIGNATURES = {
@@ -60,6 +61,26 @@ SIGNATURES = {
     "rt_bind_image": (C.c_int, [_ctx, _vp]),
     "rt_compute_one_shader": (C.c_int, [_ctx, _vp, C.c_int, C.c_int, _fp]),
     "rt_compute_two_shaders": (C.c_int, [_ctx, _vp, C.c_int, C.c_int, C.c_int, _fp]),
+    "rt_group_create": (C.c_int, [C.c_int, C.POINTER(C.c_int), C.POINTER(rt_config), C.POINTER(C.c_int),
+                                  C.POINTER(_grp)]),
+    "rt_group_destroy": (C.c_int, [_grp]),
+    "rt_group_size": (C.c_int, [_grp]),
+    "rt_group_bounds": (C.c_int, [_grp, C.POINTER(C.c_int)]),
+    "rt_group_set_bounds": (C.c_int, [_grp, C.POINTER(C.c_int)]),
+    "rt_group_strip": (_ctx, [_grp, C.c_int]),
+    "rt_group_last_hip_error": (C.c_int, [_grp]),
+    "rt_group_enable_pipelining": (C.c_int, [_grp, C.c_int]),
+    "rt_group_bind_frame": (C.c_int, [_grp, _vp]),
+    "rt_group_frame_device_ptr": (_vp, [_grp]),
+    "rt_group_upload_header": (C.c_int, [_grp, _vp, C.c_size_t]),
+    "rt_group_dispatch": (C.c_int, [_grp, C.c_int, C.c_int]),
+    "rt_group_compute_frames": (C.c_int, [_grp, _fp, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int]),
+    "rt_group_synchronize": (C.c_int, [_grp]),
+    "rt_group_download_image": (C.c_int, [_grp, _fp]),
+    "rt_group_balance": (C.c_int, [_grp, _fp, C.c_int, C.c_int, C.POINTER(C.c_double)]),
+    "rt_plan_strips": (C.c_int, [C.POINTER(C.c_double), C.c_int, C.c_int, C.POINTER(C.c_int)]),
+    "rt_calibrate_row_cost": (C.c_int, [C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_int), C.c_int,
+                                        C.POINTER(C.c_double)]),
     "rt_enable_timing": (C.c_int, [_ctx, C.c_int]),
     "rt_kernel_stats": (C.c_int, [_ctx, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]),
     "rt_reset_stats": (C.c_int, [_ctx]),

@@ -1,0 +1,502 @@
+// rt_group.cpp — multi-device row strips behind the C ABI (include/rt/abi.h, rt_group_*).
+//
+// The reference renders one frame on one GPU: compute() (src/main.cpp:553-578) dispatches
+// glDispatchCompute(WIDTH, HEIGHT, 1) and the blit reads the whole image (783-797).  Every
+// pixel is independent, so here one process drives n strip contexts (rt_ctx, one per row
+// strip, each on its own device, or several on one device) and assembles their image strips
+// into one [H][W] rgba32f frame on the root device (devices[0]):
+//   - a strip on the root device renders straight into its rows of the frame (rt_bind_image);
+//   - a strip on another device renders into its own image and copies it into the frame with
+//     one device-to-device copy over xGMI (peer access enabled), enqueued on the strip's output
+//     stream right behind the pass that writes it (the post-process when pipelined), so frame
+//     k's copy overlaps frame k+1's trace passes.
+// Each strip keeps its own g-buffer ring for its rows plus a 1-row halo (rt_create), so no
+// strip reads another's data: the copies into the frame are the only transfers.
+// One host thread per strip enqueues its strip's work, so the per-frame host cost does not add
+// up over the strips.  Strip bounds are cost-balanced (rt_group_balance): one probe frame with
+// per-row work counters, then calibration passes that time each strip and rescale the profile
+// (rt_plan_strips / rt_calibrate_row_cost, the host-only planner also used by the
+// torch.distributed path in real_time_ray_tracer_amd/dist.py).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "../../include/rt/abi.h"
+
+namespace {
+
+// n persistent worker threads; run(f) calls f(i) on worker i for every i and returns the
+// first error status (or RT_OK).
+class Workers {
+ public:
+  explicit Workers(int n) : rc_(n, RT_OK) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
+  }
+  ~Workers() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int run(const std::function<int(int)>& f) {
+    const int n = (int)th_.size();
+    if (n == 1) return f(0);
+    std::unique_lock<std::mutex> l(m_);
+    job_ = &f;
+    pending_ = n;
+    ++gen_;
+    cv_.notify_all();
+    done_.wait(l, [&] { return pending_ == 0; });
+    job_ = nullptr;
+    for (int r : rc_)
+      if (r < 0) return r;
+    return RT_OK;
+  }
+
+ private:
+  void loop(int i) {
+    long seen = 0;
+    std::unique_lock<std::mutex> l(m_);
+    for (;;) {
+      cv_.wait(l, [&] { return quit_ || gen_ != seen; });
+      if (quit_) return;
+      seen = gen_;
+      const std::function<int(int)>* f = job_;
+      l.unlock();
+      const int r = (*f)(i);
+      l.lock();
+      rc_[i] = r;
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<int(int)>* job_ = nullptr;
+  long gen_ = 0;
+  int pending_ = 0;
+  bool quit_ = false;
+  std::vector<int> rc_;
+};
+
+bool valid_bounds(const int* b, int n, int H) {
+  if (b[0] != 0 || b[n] != H) return false;
+  for (int i = 0; i < n; ++i)
+    if (b[i + 1] <= b[i]) return false;
+  return true;
+}
+
+}  // namespace
+
+struct rt_group {
+  int n = 0;
+  std::vector<int> devices;
+  rt_config cfg{};
+  std::vector<int> bounds;
+  bool pipelined = false;
+  std::vector<rt_ctx*> ctx;
+  float4* frame_own = nullptr;  // [H][W] on devices[0]
+  float4* frame = nullptr;      // the bound frame (own or the caller's)
+  std::vector<float> header;    // the group's copy of the SSBO prefix
+  std::vector<std::vector<float>> strip_header;  // per-strip copies for the worker loops
+  std::vector<char> header_dirty;
+  bool have_header = false;
+  Workers* workers = nullptr;
+  int last_hip = 0;
+};
+
+namespace {
+
+bool on_root(const rt_group* g, int i) { return g->devices[i] == g->devices[0]; }
+
+void destroy_strips(rt_group* g) {
+  for (auto*& c : g->ctx)
+    if (c) {
+      rt_destroy(c);
+      c = nullptr;
+    }
+}
+
+int bind_strips(rt_group* g) {
+  const int W = g->cfg.width;
+  for (int i = 0; i < g->n; ++i) {
+    int rc = rt_bind_image(g->ctx[i], on_root(g, i) ? (void*)(g->frame + (size_t)g->bounds[i] * W) : nullptr);
+    if (rc != RT_OK) return rc;
+  }
+  return RT_OK;
+}
+
+// (Re)create the strip contexts for g->bounds (fresh g-buffer rings).
+int make_strips(rt_group* g) {
+  destroy_strips(g);
+  g->ctx.assign(g->n, nullptr);
+  for (int i = 0; i < g->n; ++i) {
+    rt_config c = g->cfg;
+    c.row_begin = g->bounds[i];
+    c.row_end = g->bounds[i + 1];
+    int rc = rt_create(g->devices[i], &c, &g->ctx[i]);
+    if (rc == RT_OK && g->pipelined) rc = rt_enable_pipelining(g->ctx[i], 1, nullptr);
+    if (rc != RT_OK) {
+      destroy_strips(g);
+      return rc;
+    }
+  }
+  std::fill(g->header_dirty.begin(), g->header_dirty.end(), 1);
+  return bind_strips(g);
+}
+
+// The image copy of strip i into its frame rows (strips off the root device), on the strip's
+// output stream behind the pass that wrote the image.
+int copy_strip(rt_group* g, int i) {
+  if (on_root(g, i)) return RT_OK;
+  const int W = g->cfg.width;
+  const size_t bytes = (size_t)(g->bounds[i + 1] - g->bounds[i]) * W * sizeof(float4);
+  hipError_t e = hipSetDevice(g->devices[i]);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(g->frame + (size_t)g->bounds[i] * W, rt_image_device_ptr(g->ctx[i]), bytes,
+                       hipMemcpyDeviceToDevice, (hipStream_t)rt_get_output_stream(g->ctx[i]));
+  if (e != hipSuccess) {
+    g->last_hip = (int)e;
+    return RT_E_HIP;
+  }
+  return RT_OK;
+}
+
+// n frames of the render loop (src/main.cpp:763-781) on strip i, as rt_compute_frames does,
+// each followed by the strip's copy into the frame.
+int strip_frames(rt_group* g, int i, float* hdr, int mode, int frame, int n, uint64_t seed, int light) {
+  const int S = g->cfg.num_shapes, spp = g->cfg.spp;
+  const size_t bytes = rt_header_bytes(S, spp);
+  for (int k = 0; k < n; ++k) {
+    int rc = (mode == RT_MODE_AO_PP || mode == RT_MODE_AO) ? rt_fill_rand_buffer(hdr, S, spp, seed + (uint64_t)k)
+                                                           : rt_moving_light(hdr, light);
+    if (rc != RT_OK) return rc;
+    const float mz = hdr[RT_HDR_MODE * 4 + 2];
+    if (!(mz >= 0.0f && mz < (float)(S + 1))) return RT_E_INVAL;
+    rc = rt_set_mode(hdr, frame, (int)mz);
+    if (rc == RT_OK) rc = rt_upload_header(g->ctx[i], hdr, bytes);
+    if (rc != RT_OK) return rc;
+    frame = rt_dispatch(g->ctx[i], mode, frame);
+    if (frame < 0) return frame;
+    rc = copy_strip(g, i);
+    if (rc != RT_OK) return rc;
+  }
+  return frame;
+}
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_plan_strips(const double* row_cost, int H, int n, int* bounds) {
+  if (!row_cost || !bounds || H <= 0 || n <= 0 || n > H) return RT_E_INVAL;
+  double mx = 0.0;
+  for (int y = 0; y < H; ++y) {
+    if (!(row_cost[y] >= 0.0)) return RT_E_INVAL;  // negative or NaN
+    mx = std::max(mx, row_cost[y]);
+  }
+  // a tiny per-row floor, so zero-cost rows still split evenly
+  const double eps = 1e-9 * std::max(1.0, mx);
+  std::vector<double> cum((size_t)H + 1, 0.0);
+  for (int y = 0; y < H; ++y) cum[y + 1] = cum[y] + (row_cost[y] + eps);
+  const double total = cum[H];
+  bounds[0] = 0;
+  for (int i = 1; i < n; ++i) {
+    // first prefix index whose cumulative cost reaches i/n of the total
+    int y = (int)(std::lower_bound(cum.begin(), cum.end(), total * i / n) - cum.begin());
+    y = std::max(y, bounds[i - 1] + 1);
+    y = std::min(y, H - (n - i));
+    bounds[i] = y;
+  }
+  bounds[n] = H;
+  return RT_OK;
+}
+
+int rt_calibrate_row_cost(double* row_cost, int H, const int* bounds, int n, const double* strip_ms) {
+  if (!row_cost || !bounds || !strip_ms || H <= 0 || n <= 0 || !valid_bounds(bounds, n, H)) return RT_E_INVAL;
+  for (int i = 0; i < n; ++i) {
+    const int a = bounds[i], b = bounds[i + 1];
+    double tot = 0.0;
+    for (int y = a; y < b; ++y) tot += row_cost[y];
+    for (int y = a; y < b; ++y) row_cost[y] = tot > 0.0 ? row_cost[y] * (strip_ms[i] / tot) : strip_ms[i] / (b - a);
+  }
+  return RT_OK;
+}
+
+int rt_group_create(int n, const int* devices, const rt_config* cfg, const int* bounds, rt_group** out) {
+  if (!out) return RT_E_INVAL;
+  *out = nullptr;
+  if (n <= 0 || !devices || !cfg || cfg->height <= 0 || cfg->width <= 0 || n > cfg->height) return RT_E_INVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_E_NODEV;
+  for (int i = 0; i < n; ++i)
+    if (devices[i] < 0 || devices[i] >= ndev) return RT_E_NODEV;
+  rt_group* g = new (std::nothrow) rt_group();
+  if (!g) return RT_E_NOMEM;
+  g->n = n;
+  g->devices.assign(devices, devices + n);
+  g->cfg = *cfg;
+  g->cfg.row_begin = g->cfg.row_end = 0;
+  const int H = cfg->height, W = cfg->width;
+  g->bounds.resize(n + 1);
+  if (bounds) {
+    if (!valid_bounds(bounds, n, H)) {
+      delete g;
+      return RT_E_INVAL;
+    }
+    std::copy(bounds, bounds + n + 1, g->bounds.begin());
+  } else {
+    for (int i = 0; i <= n; ++i) g->bounds[i] = (int)(((long long)i * H + n / 2) / n);
+  }
+  g->header.assign(rt_header_bytes(std::max(0, cfg->num_shapes), std::max(1, cfg->spp)) / 4, 0.0f);
+  g->strip_header.assign(n, g->header);
+  g->header_dirty.assign(n, 1);
+  // peer access root <-> every other device (the strip copies go over xGMI)
+  for (int i = 1; i < n; ++i) {
+    const int d = g->devices[i], r = g->devices[0];
+    if (d == r) continue;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, d, r) == hipSuccess && can && hipSetDevice(d) == hipSuccess) {
+      hipError_t e = hipDeviceEnablePeerAccess(r, 0);
+      if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+    }
+  }
+  hipError_t e = hipSetDevice(g->devices[0]);
+  if (e == hipSuccess) e = hipMalloc(&g->frame_own, (size_t)H * W * sizeof(float4));
+  if (e == hipSuccess) e = hipMemset(g->frame_own, 0, (size_t)H * W * sizeof(float4));
+  if (e != hipSuccess) {
+    if (g->frame_own) (void)hipFree(g->frame_own);
+    delete g;
+    return e == hipErrorOutOfMemory ? RT_E_NOMEM : RT_E_HIP;
+  }
+  g->frame = g->frame_own;
+  int rc = make_strips(g);
+  if (rc != RT_OK) {
+    (void)hipFree(g->frame_own);
+    delete g;
+    return rc;
+  }
+  g->workers = new (std::nothrow) Workers(n);
+  if (!g->workers) {
+    rt_group_destroy(g);
+    return RT_E_NOMEM;
+  }
+  *out = g;
+  return RT_OK;
+}
+
+int rt_group_destroy(rt_group* g) {
+  if (!g) return RT_E_INVAL;
+  for (auto* c : g->ctx)
+    if (c) (void)rt_synchronize(c);
+  delete g->workers;
+  destroy_strips(g);
+  if (g->frame_own) {
+    (void)hipSetDevice(g->devices[0]);
+    (void)hipFree(g->frame_own);
+  }
+  delete g;
+  return RT_OK;
+}
+
+int rt_group_size(rt_group* g) { return g ? g->n : RT_E_INVAL; }
+
+int rt_group_bounds(rt_group* g, int* bounds) {
+  if (!g || !bounds) return RT_E_INVAL;
+  std::copy(g->bounds.begin(), g->bounds.end(), bounds);
+  return RT_OK;
+}
+
+int rt_group_set_bounds(rt_group* g, const int* bounds) {
+  if (!g || !bounds || !valid_bounds(bounds, g->n, g->cfg.height)) return RT_E_INVAL;
+  for (auto* c : g->ctx) {
+    int rc = rt_synchronize(c);
+    if (rc != RT_OK) return rc;
+  }
+  std::copy(bounds, bounds + g->n + 1, g->bounds.begin());
+  return make_strips(g);
+}
+
+rt_ctx* rt_group_strip(rt_group* g, int i) { return (g && i >= 0 && i < g->n) ? g->ctx[i] : nullptr; }
+
+int rt_group_last_hip_error(rt_group* g) {
+  if (!g) return 0;
+  if (g->last_hip) return g->last_hip;
+  for (auto* c : g->ctx)
+    if (c && rt_last_hip_error(c)) return rt_last_hip_error(c);
+  return 0;
+}
+
+int rt_group_enable_pipelining(rt_group* g, int on) {
+  if (!g) return RT_E_INVAL;
+  g->pipelined = on != 0;
+  for (auto* c : g->ctx) {
+    int rc = rt_enable_pipelining(c, on, nullptr);
+    if (rc != RT_OK) return rc;
+  }
+  return RT_OK;
+}
+
+int rt_group_bind_frame(rt_group* g, void* device_ptr) {
+  if (!g) return RT_E_INVAL;
+  for (auto* c : g->ctx) {  // the frame in use may still be written
+    int rc = rt_synchronize(c);
+    if (rc != RT_OK) return rc;
+  }
+  g->frame = device_ptr ? (float4*)device_ptr : g->frame_own;
+  return bind_strips(g);
+}
+
+void* rt_group_frame_device_ptr(rt_group* g) { return g ? (void*)g->frame : nullptr; }
+
+int rt_group_upload_header(rt_group* g, const void* header, size_t bytes) {
+  if (!g || !header) return RT_E_INVAL;
+  const int S = g->cfg.num_shapes;
+  if (bytes != rt_header_bytes(S, g->cfg.spp)) return RT_E_INVAL;
+  const float mz = ((const float*)header)[RT_HDR_MODE * 4 + 2];
+  if (!(mz >= 0.0f && mz < (float)(S + 1))) return RT_E_INVAL;
+  std::memcpy(g->header.data(), header, bytes);
+  std::fill(g->header_dirty.begin(), g->header_dirty.end(), 1);
+  g->have_header = true;
+  return RT_OK;
+}
+
+int rt_group_dispatch(rt_group* g, int mode, int frame) {
+  if (!g) return RT_E_INVAL;
+  if (!g->have_header) return RT_E_STATE;
+  if (mode < RT_MODE_AO_PP || mode > RT_MODE_PHONG_REFL || frame < 0 || frame >= g->cfg.num_frames)
+    return RT_E_INVAL;
+  const size_t bytes = g->header.size() * sizeof(float);
+  int rc = g->workers->run([&](int i) -> int {
+    if (g->header_dirty[i]) {
+      int r = rt_upload_header(g->ctx[i], g->header.data(), bytes);
+      if (r != RT_OK) return r;
+      g->header_dirty[i] = 0;
+    }
+    int f = rt_dispatch(g->ctx[i], mode, frame);
+    if (f < 0) return f;
+    return copy_strip(g, i);
+  });
+  if (rc != RT_OK) return rc;
+  return (frame + 1) % g->cfg.num_frames;
+}
+
+int rt_group_compute_frames(rt_group* g, float* header, int mode, int frame, int n, uint64_t rand_seed,
+                            int light_movement) {
+  if (!g || !header || n < 0 || mode < RT_MODE_AO_PP || mode > RT_MODE_PHONG_REFL) return RT_E_INVAL;
+  if (frame < 0 || frame >= g->cfg.num_frames) return RT_E_INVAL;
+  const size_t nf = g->header.size();
+  std::vector<int> next(g->n, frame);
+  int rc = g->workers->run([&](int i) -> int {
+    std::vector<float>& h = g->strip_header[i];
+    std::memcpy(h.data(), header, nf * sizeof(float));
+    int f = strip_frames(g, i, h.data(), mode, frame, n, rand_seed, light_movement);
+    if (f < 0) return f;
+    next[i] = f;
+    return RT_OK;
+  });
+  if (rc != RT_OK) return rc;
+  std::memcpy(header, g->strip_header[0].data(), nf * sizeof(float));  // as the host loop leaves it
+  std::memcpy(g->header.data(), header, nf * sizeof(float));
+  std::fill(g->header_dirty.begin(), g->header_dirty.end(), 0);  // every strip holds this header
+  g->have_header = true;
+  return next[0];
+}
+
+int rt_group_synchronize(rt_group* g) {
+  if (!g) return RT_E_INVAL;
+  for (auto* c : g->ctx) {
+    int rc = rt_synchronize(c);
+    if (rc != RT_OK) return rc;
+  }
+  return RT_OK;
+}
+
+int rt_group_download_image(rt_group* g, float* image) {
+  if (!g || !image) return RT_E_INVAL;
+  int rc = rt_group_synchronize(g);
+  if (rc != RT_OK) return rc;
+  hipError_t e = hipSetDevice(g->devices[0]);
+  if (e == hipSuccess)
+    e = hipMemcpy(image, g->frame, (size_t)g->cfg.height * g->cfg.width * sizeof(float4), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) {
+    g->last_hip = (int)e;
+    return RT_E_HIP;
+  }
+  return RT_OK;
+}
+
+int rt_group_balance(rt_group* g, const float* header, int mode, int rounds, double* strip_ms) {
+  if (!g || !header || mode < RT_MODE_AO_PP || mode > RT_MODE_PHONG_REFL || rounds < 0) return RT_E_INVAL;
+  const int H = g->cfg.height, n = g->n;
+  const size_t nf = g->header.size();
+  std::vector<float> h(header, header + nf);
+  // 1. one probe frame with per-row work counters on every strip -> the frame's cost profile
+  std::vector<double> cost(H, 0.0);
+  int rc = g->workers->run([&](int i) -> int {
+    std::vector<float> hh(h);
+    int r = rt_enable_counters(g->ctx[i], 2);
+    if (r != RT_OK) return r;
+    int f = strip_frames(g, i, hh.data(), mode, 0, 1, 7000, 0);
+    if (f < 0) return f;
+    std::vector<uint64_t> rows(g->bounds[i + 1] - g->bounds[i]);
+    r = rt_read_row_counters(g->ctx[i], rows.data(), 1);
+    if (r == RT_OK) r = rt_enable_counters(g->ctx[i], 0);
+    for (size_t k = 0; k < rows.size(); ++k) cost[g->bounds[i] + k] = (double)rows[k];
+    return r;
+  });
+  if (rc != RT_OK) return rc;
+  std::vector<int> b(n + 1);
+  rc = rt_plan_strips(cost.data(), H, n, b.data());
+  if (rc != RT_OK) return rc;
+  // 2. calibration: time every strip of the plan alone, as the frame loop renders it (wall
+  // clock of 16 frames after 8, gather copy included), rescale the profile so each strip's
+  // total is its time, re-plan; keep the best measured plan
+  std::vector<int> best = b;
+  double best_ms = -1.0;
+  std::vector<double> best_t(n, 0.0), t(n, 0.0);
+  for (int it = 0; it < std::max(1, rounds); ++it) {
+    rc = rt_group_set_bounds(g, b.data());
+    if (rc != RT_OK) return rc;
+    for (int i = 0; i < n && rc == RT_OK; ++i) {  // one strip at a time (strips may share a device)
+      std::vector<float> hh(h);
+      int f = strip_frames(g, i, hh.data(), mode, 0, 8, 7000, 0);
+      if (f >= 0) f = rt_synchronize(g->ctx[i]) == RT_OK ? f : RT_E_HIP;
+      const double t0 = now_ms();
+      if (f >= 0) f = strip_frames(g, i, hh.data(), mode, f, 16, 7008, 0);
+      if (f >= 0 && rt_synchronize(g->ctx[i]) != RT_OK) f = RT_E_HIP;
+      if (f < 0) rc = f;
+      t[i] = (now_ms() - t0) / 16.0;
+    }
+    if (rc != RT_OK) return rc;
+    const double mx = *std::max_element(t.begin(), t.end());
+    if (best_ms < 0.0 || mx < best_ms) {
+      best_ms = mx;
+      best = b;
+      best_t = t;
+    }
+    if (it + 1 < rounds) {
+      rc = rt_calibrate_row_cost(cost.data(), H, b.data(), n, t.data());
+      if (rc == RT_OK) rc = rt_plan_strips(cost.data(), H, n, b.data());
+      if (rc != RT_OK) return rc;
+    }
+  }
+  if (strip_ms) std::copy(best_t.begin(), best_t.end(), strip_ms);
+  return rt_group_set_bounds(g, best.data());  // fresh rings on the chosen plan
+}
+
+}  // extern "C"

@@ -7,6 +7,10 @@
 //
 //   rt_headless [--width W] [--height H] [--objects N] [--spp A] [--mode 1..4] [--frames K]
 //               [--scene synthetic|1|5|6] [--seed S] [--device D] [--ppm out.ppm] [--pipeline 0|1]
+//               [--strips G] [--devices d0,d1,...] [--balance ROUNDS]
+// --strips G > 1 renders the frame as G row strips through the rt_group_* entry points: strip i
+// on device devices[i % #devices] (default: every visible device in turn, or --device), cost-
+// balanced with --balance ROUNDS timed plans (0: equal strips), assembled on the first device.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -41,9 +45,48 @@ static void write_ppm(const char* path, const std::vector<float>& img, int W, in
   std::fclose(f);
 }
 
+// The frame as `strips` row strips over the devices in `devlist` (rt_group_*).
+static int run_strips(const rt_config& cfg, std::vector<float>& header, int mode, int frames, int pipeline,
+                      int strips, const std::string& devlist, int device, int balance, const std::string& ppm) {
+  std::vector<int> devs;
+  for (size_t p = 0; p < devlist.size();) {
+    size_t q = devlist.find(',', p);
+    if (q == std::string::npos) q = devlist.size();
+    devs.push_back(std::atoi(devlist.substr(p, q - p).c_str()));
+    p = q + 1;
+  }
+  if (devs.empty()) devs.push_back(device);
+  std::vector<int> sd(strips);
+  for (int i = 0; i < strips; ++i) sd[i] = devs[i % devs.size()];
+  rt_group* g = nullptr;
+  check(rt_group_create(strips, sd.data(), &cfg, nullptr, &g), "rt_group_create");
+  if (pipeline) check(rt_group_enable_pipelining(g, 1), "rt_group_enable_pipelining");
+  std::vector<double> strip_ms(strips, 0.0);
+  if (balance > 0) check(rt_group_balance(g, header.data(), mode, balance, strip_ms.data()), "rt_group_balance");
+  std::vector<int> b(strips + 1);
+  check(rt_group_bounds(g, b.data()), "rt_group_bounds");
+  std::printf("strips:");
+  for (int i = 0; i < strips; ++i) std::printf(" [%d,%d)@%d", b[i], b[i + 1], sd[i]);
+  std::printf("\n");
+  auto t0 = std::chrono::steady_clock::now();
+  check(rt_group_compute_frames(g, header.data(), mode, 0, frames, 7000, 0), "rt_group_compute_frames");
+  check(rt_group_synchronize(g), "rt_group_synchronize");
+  double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const int W = cfg.width, H = cfg.height, A = cfg.spp;
+  std::printf("%dx%d spp=%d mode=%d %d strips%s: %.3f ms/frame (wall), %.1f Mrays/s\n", W, H, A, mode, strips,
+              pipeline ? " pipelined" : "", wall / frames, (double)W * H * (mode <= 2 ? A : 1) * frames / (wall * 1e3));
+  if (!ppm.empty()) {
+    std::vector<float> img((size_t)W * H * 4);
+    check(rt_group_download_image(g, img.data()), "rt_group_download_image");
+    write_ppm(ppm.c_str(), img, W, H);
+  }
+  rt_group_destroy(g);
+  return 0;
+}
+
 int main(int argc, char** argv) {
-  int W = 440, H = 330, N = 5, A = 4, mode = 1, frames = 8, device = 0, pipeline = 0;
-  std::string scene = "1", ppm;
+  int W = 440, H = 330, N = 5, A = 4, mode = 1, frames = 8, device = 0, pipeline = 0, strips = 1, balance = 0;
+  std::string scene = "1", ppm, devlist;
   unsigned long long seed = 1234;
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string k = argv[i], v = argv[i + 1];
@@ -58,6 +101,9 @@ int main(int argc, char** argv) {
     else if (k == "--device") device = std::atoi(v.c_str());
     else if (k == "--ppm") ppm = v;
     else if (k == "--pipeline") pipeline = std::atoi(v.c_str());
+    else if (k == "--strips") strips = std::atoi(v.c_str());
+    else if (k == "--devices") devlist = v;
+    else if (k == "--balance") balance = std::atoi(v.c_str());
     else { std::fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
   }
   const float aspect = (W * 3 == H * 4) ? 1.333333f : 1.777777f;  // main.cpp:39-40
@@ -67,6 +113,7 @@ int main(int argc, char** argv) {
   else check(rt_init_scene(header.data(), S, A, std::atoi(scene.c_str()), aspect), "rt_init_scene");
 
   rt_config cfg{W, H, S, A, RT_NUM_FRAMES, RT_RECURSION_DEPTH, 0, 0};
+  if (strips > 1) return run_strips(cfg, header, mode, frames, pipeline, strips, devlist, device, balance, ppm);
   rt_ctx* ctx = nullptr;
   check(rt_create(device, &cfg, &ctx), "rt_create");
   check(rt_enable_timing(ctx, 1), "rt_enable_timing");

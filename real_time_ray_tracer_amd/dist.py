@@ -22,20 +22,12 @@ def equal_bounds(H: int, n: int) -> list[int]:
     return [round(i * H / n) for i in range(n + 1)]
 
 
-def balanced_bounds(row_cost: np.ndarray, n: int, min_rows: int = 1) -> list[int]:
-    """Contiguous strips of (nearly) equal total cost.  row_cost[y] >= 0 for every frame row."""
-    H = len(row_cost)
-    c = np.asarray(row_cost, np.float64) + 1e-9 * max(1.0, float(np.max(row_cost)) if H else 1.0)
-    cum = np.concatenate([[0.0], np.cumsum(c)])
-    total = cum[-1]
-    b = [0]
-    for i in range(1, n):
-        y = int(np.searchsorted(cum, total * i / n))
-        y = max(y, b[-1] + min_rows)
-        y = min(y, H - (n - i) * min_rows)
-        b.append(y)
-    b.append(H)
-    return b
+def balanced_bounds(row_cost: np.ndarray, n: int) -> list[int]:
+    """Contiguous strips of (nearly) equal total cost, row_cost[y] >= 0 for every frame row:
+    the C ABI's host-only planner (rt_plan_strips), shared with the one-process rt_group path."""
+    from .host import plan_strips
+
+    return plan_strips(row_cost, n)
 
 
 def strip_cost(bounds: list[int], row_cost: np.ndarray) -> list[float]:
@@ -45,19 +37,10 @@ def strip_cost(bounds: list[int], row_cost: np.ndarray) -> list[float]:
 def calibrate_row_cost(bounds: list[int], row_cost: np.ndarray, strip_time: list[float]) -> np.ndarray:
     """Rescale the modelled per-row cost so every strip's total equals its measured time
     (keeping the row shape inside each strip): corrects the cost model (setup vs test cost,
-    per-rank overheads) before a second balancing pass."""
-    c = np.asarray(row_cost, np.float64).copy()
-    for i in range(len(bounds) - 1):
-        a, b = bounds[i], bounds[i + 1]
-        tot = float(np.sum(c[a:b]))
-        t = float(strip_time[i])
-        if b <= a:
-            continue
-        if tot > 0:
-            c[a:b] *= t / tot
-        else:
-            c[a:b] = t / (b - a)
-    return c
+    per-rank overheads) before a second balancing pass (rt_calibrate_row_cost)."""
+    from .host import calibrate_row_cost as _cal
+
+    return _cal(bounds, row_cost, strip_time)
 
 
 def imbalance(strip_time: list[float]) -> float:

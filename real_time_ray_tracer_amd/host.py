@@ -329,6 +329,122 @@ class Renderer:
         return out
 
 
+class StripGroup:
+    """Row strips of one frame on several devices in one process (rt_group_*, the C-ABI
+    counterpart of dist.py's one-process-per-GPU path): strip i = rows [bounds[i], bounds[i+1])
+    on devices[i]; the image strips are assembled into one [H][W] frame on devices[0]."""
+
+    def __init__(self, width: int, height: int, num_shapes: int, spp: int, devices, bounds=None,
+                 num_frames: int = 8, max_depth: int = 20):
+        self._lib = _lib.load()
+        self.W, self.H, self.S, self.AA, self.F = width, height, num_shapes, spp, num_frames
+        devs = [int(d) for d in devices]
+        self.n = len(devs)
+        cfg = _lib.rt_config(width, height, num_shapes, spp, num_frames, max_depth, 0, 0)
+        dv = (C.c_int * self.n)(*devs)
+        bd = None if bounds is None else (C.c_int * (self.n + 1))(*[int(b) for b in bounds])
+        g = C.c_void_p()
+        _check(self._lib.rt_group_create(self.n, dv, C.byref(cfg), bd, C.byref(g)), "rt_group_create")
+        self.g = g
+
+    def close(self):
+        if self.g:
+            self._lib.rt_group_destroy(self.g)
+            self.g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _c(self, rc, what):
+        if rc < 0:
+            raise RtError(rc, what, self._lib.rt_group_last_hip_error(self.g) if self.g else 0)
+        return rc
+
+    @property
+    def bounds(self) -> list[int]:
+        b = (C.c_int * (self.n + 1))()
+        self._c(self._lib.rt_group_bounds(self.g, b), "rt_group_bounds")
+        return list(b)
+
+    def set_bounds(self, bounds):
+        self._c(self._lib.rt_group_set_bounds(self.g, (C.c_int * (self.n + 1))(*[int(b) for b in bounds])),
+                "rt_group_set_bounds")
+
+    def strip_ctx(self, i: int):
+        return self._lib.rt_group_strip(self.g, i)
+
+    def strip_kernel_stats(self, i: int, program: int) -> tuple[int, float]:
+        n, ms = C.c_int(), C.c_double()
+        _check(self._lib.rt_kernel_stats(self.strip_ctx(i), program, C.byref(n), C.byref(ms)), "rt_kernel_stats")
+        return n.value, ms.value
+
+    def enable_pipelining(self, on: bool = True):
+        self._c(self._lib.rt_group_enable_pipelining(self.g, int(bool(on))), "rt_group_enable_pipelining")
+
+    def bind_frame(self, device_ptr: int | None):
+        self._c(self._lib.rt_group_bind_frame(self.g, C.c_void_p(device_ptr) if device_ptr else None),
+                "rt_group_bind_frame")
+
+    def frame_device_ptr(self) -> int:
+        return self._lib.rt_group_frame_device_ptr(self.g) or 0
+
+    def upload_header(self, header: Header):
+        assert header.S == self.S and header.AA == self.AA
+        self._c(self._lib.rt_group_upload_header(self.g, header.data.ctypes.data_as(C.c_void_p), header.data.nbytes),
+                "rt_group_upload_header")
+
+    def dispatch(self, mode: int, frame: int) -> int:
+        return self._c(self._lib.rt_group_dispatch(self.g, mode, frame), f"rt_group_dispatch(mode {mode})")
+
+    def compute_frames(self, header: Header, mode: int, frame: int, n: int, rand_seed: int = 7000,
+                       light_movement: bool = False) -> int:
+        return self._c(self._lib.rt_group_compute_frames(self.g, header._p(), mode, frame, n, rand_seed,
+                                                         int(bool(light_movement))), "rt_group_compute_frames")
+
+    def synchronize(self):
+        self._c(self._lib.rt_group_synchronize(self.g), "rt_group_synchronize")
+
+    def image(self) -> np.ndarray:
+        im = np.empty((self.H, self.W, 4), np.float32)
+        self._c(self._lib.rt_group_download_image(self.g, fptr(im)), "rt_group_download_image")
+        return im
+
+    def balance(self, header: Header, mode: int, rounds: int = 3) -> list[float]:
+        """Cost-balance the strips (probe frame + `rounds` timed plans); returns the kept plan's
+        per-strip ms per frame.  The strips restart with fresh rings."""
+        ms = (C.c_double * self.n)()
+        self._c(self._lib.rt_group_balance(self.g, header._p(), mode, rounds, ms), "rt_group_balance")
+        return list(ms)
+
+
+def plan_strips(row_cost, n: int) -> list[int]:
+    """rt_plan_strips: contiguous strips of nearly equal total cost (host only)."""
+    c = np.ascontiguousarray(row_cost, np.float64)
+    b = (C.c_int * (n + 1))()
+    _check(_lib.load().rt_plan_strips(c.ctypes.data_as(C.POINTER(C.c_double)), c.size, n, b), "rt_plan_strips")
+    return list(b)
+
+
+def calibrate_row_cost(bounds, row_cost, strip_ms) -> np.ndarray:
+    """rt_calibrate_row_cost: rescale the profile so each strip's total is its measured time."""
+    c = np.array(row_cost, np.float64)
+    n = len(bounds) - 1
+    b = (C.c_int * (n + 1))(*[int(x) for x in bounds])
+    t = np.ascontiguousarray(strip_ms, np.float64)
+    _check(_lib.load().rt_calibrate_row_cost(c.ctypes.data_as(C.POINTER(C.c_double)), c.size, b, n,
+                                             t.ctypes.data_as(C.POINTER(C.c_double))), "rt_calibrate_row_cost")
+    return c
+
+
 class FrameDriver:
     """compute() of src/main.cpp:553-578 with its per-frame host updates: the frame ring
     (static frame_num, 555/619), fill_rand_buffer for AO modes (seeded: 7000 + frame count),

@@ -135,3 +135,31 @@ def test_calibration_corrects_a_wrong_cost_model():
     # an empty-cost strip is spread uniformly, not divided by zero
     c = calibrate_row_cost([0, 2, 4], np.zeros(4), [1.0, 3.0])
     assert np.allclose(c, [0.5, 0.5, 1.5, 1.5])
+
+
+def test_c_planner_matches_numpy_restatement_and_rejects_bad_input():
+    """rt_plan_strips (host-only C ABI) against a numpy restatement of the same rule, and its
+    error paths; rt_calibrate_row_cost keeps each strip's row shape."""
+    from real_time_ray_tracer_amd import RtError
+    from real_time_ray_tracer_amd.host import calibrate_row_cost, plan_strips
+
+    rng = np.random.default_rng(3)
+    for H, n in [(2160, 8), (1080, 3), (17, 17), (100, 1)]:
+        cost = rng.gamma(0.7, 5.0, H) * (rng.random(H) > 0.2)
+        c = cost + 1e-9 * max(1.0, cost.max())
+        cum = np.r_[0.0, np.cumsum(c)]
+        want = [0]
+        for i in range(1, n):
+            y = int(np.searchsorted(cum, cum[-1] * i / n))
+            want.append(min(max(y, want[-1] + 1), H - (n - i)))
+        want.append(H)
+        assert plan_strips(cost, n) == want
+    for bad in [(np.ones(4), 5), (np.r_[1.0, -1.0, 1.0], 2), (np.r_[1.0, np.nan], 1), (np.ones(4), 0)]:
+        with pytest.raises(RtError):
+            plan_strips(*bad)
+    cost = np.arange(1.0, 11.0)
+    out = calibrate_row_cost([0, 4, 10], cost, [2.0, 8.0])
+    assert np.isclose(out[:4].sum(), 2.0) and np.isclose(out[4:].sum(), 8.0)
+    assert np.allclose(out[:4] / out[0], cost[:4] / cost[0])
+    with pytest.raises(RtError):
+        calibrate_row_cost([0, 4, 4, 10], cost, [1.0, 1.0, 1.0])
