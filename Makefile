@@ -18,11 +18,12 @@ CFLAGS_ORACLE := -O3 -march=x86-64-v3 -ffp-contract=off -fopenmp -fPIC -std=c99 
 
 LIB      := $(PKG)/librtrt.so
 ORACLE   := oracle/build/librt_oracle.so
+ORACLE_NATIVE := oracle/build/librt_oracle_zen.so
 HEADLESS := build/rt_headless
 
 all: lib oracle headless
 lib: $(LIB)
-oracle: $(ORACLE)
+oracle: $(ORACLE) $(ORACLE_NATIVE)
 headless: $(HEADLESS)
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/*.h include/rt/*.h | $(OBJDIR)
@@ -34,8 +35,14 @@ $(OBJDIR)/rt_host.o: $(CSRC)/rt_host.cpp include/rt/*.h | $(OBJDIR)
 $(OBJDIR)/rt_group.o: $(CSRC)/rt_group.cpp include/rt/*.h | $(OBJDIR)
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Iinclude -c $< -o $@
 
+# BUILD_INFO: sha1 of the library's sources (+ the git commit they were built at, "+dirty" if
+# they differ from it), so measurements can name the kernel code they were taken on
 $(LIB): $(OBJDIR)/rt_kernels.o $(OBJDIR)/rt_shim.o $(OBJDIR)/rt_host.o $(OBJDIR)/rt_group.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
+	@src=$$(cat $(CSRC)/*.hip $(CSRC)/*.h $(CSRC)/rt_host.cpp $(CSRC)/rt_group.cpp include/rt/*.h Makefile | sha1sum | cut -c1-12); \
+	 commit=$$(git rev-parse --short=12 HEAD 2>/dev/null || echo unknown); \
+	 git diff --quiet HEAD -- $(CSRC) include Makefile 2>/dev/null || commit="$$commit+dirty"; \
+	 printf '{"src_sha1": "%s", "commit": "%s"}\n' "$$src" "$$commit" > $(PKG)/BUILD_INFO
 
 ABLIB := build/librtrt_ab.so
 $(OBJDIR)/ab_%.o: $(CSRC)/%.hip $(CSRC)/*.h include/rt/*.h | $(OBJDIR)
@@ -49,6 +56,11 @@ ablib: $(ABLIB)
 $(ORACLE): oracle/rt_oracle.c oracle/rt_oracle.h include/rt/layout.h
 	@mkdir -p oracle/build
 	$(CC) $(CFLAGS_ORACLE) -shared -o $@ oracle/rt_oracle.c -lm
+
+# CPU-baseline build for the GPU box's AMD EPYC (Zen 5) host cores; same source and float flags
+$(ORACLE_NATIVE): oracle/rt_oracle.c oracle/rt_oracle.h include/rt/layout.h
+	@mkdir -p oracle/build
+	$(CC) $(subst -march=x86-64-v3,-march=znver3 -mtune=znver3 -mavx512f -mavx512cd -mavx512bw -mavx512dq -mavx512vl,$(CFLAGS_ORACLE)) -shared -o $@ oracle/rt_oracle.c -lm
 
 $(HEADLESS): $(CSRC)/rt_headless.cpp $(LIB) include/rt/*.h
 	$(CXX) -O2 -std=c++17 -Iinclude -o $@ $< -L$(PKG) -lrtrt -Wl,-rpath,'$$ORIGIN/../$(PKG)'

@@ -44,10 +44,14 @@ CONFIGS = {
     # scenes with planes (not BASELINE configs: the plane path's own measurement)
     "p": (3840, 2160, 65, 16, 1, "config (d) + one ground plane (64 spheres + 1 plane = 65 objects), AO 16 spp + "
                                  "post-process (mode 1)"),
+    # diagnostic twin of "p": the plane replaced by a sphere of radius 1e4 tangent to it (same
+    # workload shape, all spheres): isolates what the plane path itself costs
+    "q": (3840, 2160, 65, 16, 1, "config p with its plane replaced by a radius-1e4 sphere tangent to it (65 spheres), "
+                                 "AO 16 spp + post-process (mode 1)"),
     "s1": (3840, 2160, 10, 16, 1, "the reference's scene1 (4 spheres + 1 plane, src/scene.h:15-65) at 3840x2160, "
                                   "AO 16 spp + post-process (mode 1)"),
 }
-CONFIG_INDEX = {"a": 0, "b": 1, "c": 2, "d": 3, "e": 4, "p": 3, "s1": 3}
+CONFIG_INDEX = {"a": 0, "b": 1, "c": 2, "d": 3, "e": 4, "p": 3, "q": 3, "s1": 3}
 
 
 def config_header(name: str):
@@ -58,9 +62,12 @@ def config_header(name: str):
     W, H, S, spp, _, _ = CONFIGS[name]
     if name == "s1":
         return Header.builtin(1, spp, aspect_for(W, H), num_shapes=S)
-    if name == "p":
+    if name in ("p", "q"):
         h = Header.synthetic(S - 1, spp, 1234 + CONFIG_INDEX[name], aspect_for(W, H), num_shapes=S)
-        h.pack_plane(S - 1, (0.0, 1.0, 0.0), -2.5, (0.45, 0.4, 0.35), reflectivity=1.0)
+        if name == "p":
+            h.pack_plane(S - 1, (0.0, 1.0, 0.0), -2.5, (0.45, 0.4, 0.35), reflectivity=1.0)
+        else:
+            h.pack_sphere(S - 1, (0.0, -10002.5, 0.0), 10000.0, (0.45, 0.4, 0.35), reflectivity=1.0)
         h.set_mode(0, S)
         return h
     return Header.synthetic(S, spp, 1234 + CONFIG_INDEX[name], aspect_for(W, H))
@@ -85,31 +92,42 @@ def cpu_baseline(cfg_name: str, target_s: float) -> dict:
     """The CPU oracle (oracle/rt_oracle.c, OpenMP over rows) on a bounded, evenly spread sample
     of rows of the same frame; both mode-1 passes for config (d)."""
     import oracle
-    from real_time_ray_tracer_amd import Header, aspect_for
 
+    oracle.select_native()
     W, H, S, spp, mode, _ = CONFIGS[cfg_name]
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     h = config_header(cfg_name)
     progs = {1: [oracle.AOP_COMPUTE, oracle.AOP_POSTPROCESSING], 2: [oracle.AO_COMPUTE],
              3: [oracle.P_COMPUTE], 4: [oracle.H_COMPUTE]}[mode]
 
-    def run_rows(rows):
+    BAND, FR = 4, 2  # bands of 4 rows (vertical neighbours for the post-process), 2 frames each
+
+    def run_bands(starts):
         t = 0.0
-        for y in rows:
-            d = oracle.dims(W, H, S, spp, gy0=int(y), gh=1)
-            buf = np.zeros(h.data.size + 3 * 8 * W * 4, np.float32)
-            buf[:h.data.size] = h.data
+        for y in starts:
+            gh = min(BAND, H - int(y))
+            d = oracle.dims(W, H, S, spp, gy0=int(y), gh=gh)
+            buf = np.zeros(h.data.size + 3 * 8 * W * gh * 4, np.float32)
+            hh = h.copy()
             t0 = time.perf_counter()
-            for p in progs:
-                oracle.run_program(buf, d, p, 0, None, nthreads=threads)
+            for k in range(FR):  # the render loop's frames: history slot k-1 is filled
+                if mode in (1, 2):
+                    hh.fill_rand_buffer(7000 + k)
+                else:
+                    hh.moving_light(False)
+                hh.set_mode(k, hh.num_objects)
+                buf[:hh.data.size] = hh.data
+                for p in progs:
+                    oracle.run_program(buf, d, p, k, None, nthreads=threads)
             t += time.perf_counter() - t0
         return t
 
-    probe = run_rows([H // 2])
-    n = int(max(2, min(H, target_s / max(probe, 1e-4))))
-    rows = [int((i + 0.5) * H / n) for i in range(n)]
-    t = run_rows(rows)
-    units = len(rows) * W * (spp if mode in (1, 2) else 1)
+    probe = run_bands([H // 2])
+    n = int(max(2, min(H // BAND, target_s / max(probe, 1e-4))))
+    starts = [min(H - BAND, int((i + 0.5) * H / n)) for i in range(n)]
+    t = run_bands(starts)
+    rows = [0] * (n * BAND)
+    units = len(rows) * W * (spp if mode in (1, 2) else 1) * FR
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -120,22 +138,37 @@ def cpu_baseline(cfg_name: str, target_s: float) -> dict:
         pass
     return {"value": round(units / t / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "cpu": model,
-            "sample": f"{len(rows)} of {H} rows (evenly spread) x {W} px x {spp if mode in (1, 2) else 1} spp, "
+            "build": oracle.lib_name(),
+            "sample": f"{n} bands of {BAND} rows (evenly spread, {len(rows)} of {H} rows) x {FR} frames x {W} px x "
+                      f"{spp if mode in (1, 2) else 1} spp, "
                       f"{'+'.join({1: 'aop_compute', 2: 'aop_postprocessing', 3: 'ao_compute', 4: 'p_compute', 5: 'h_compute'}[p] for p in progs)}, "
                       f"oracle/rt_oracle.c with {threads} OpenMP threads, {t:.1f} s; ms/frame extrapolated "
-                      f"{t / len(rows) * H * 1e3:.0f}"}
+                      f"{t / (len(rows) * FR) * H * 1e3:.0f}"}
 
 
-def load_traffic(cfg_name: str):
-    """HBM bytes per launch measured with rocprofv3 PMC passes (profiles/*_pmc.json)."""
+def build_info() -> dict:
+    """The library's source hash and commit (written by `make lib` next to librtrt.so)."""
+    try:
+        return json.loads((ROOT / "real_time_ray_tracer_amd" / "BUILD_INFO").read_text())
+    except Exception:
+        return {"src_sha1": None, "commit": None}
+
+
+def load_traffic(cfg_name: str, src_sha1):
+    """HBM bytes per launch measured with rocprofv3 PMC passes (profiles/*_pmc.json): the newest
+    file for this config, preferring one taken on this library build (same source hash)."""
+    found = []
     for p in sorted(ROOT.glob("profiles/*_pmc.json"), reverse=True):
         try:
             data = json.loads(p.read_text())
         except Exception:
             continue
         if data.get("config") == cfg_name:
-            return data, p.name
-    return None, None
+            found.append((data, p.name))
+    for data, name in found:
+        if src_sha1 and data.get("src_sha1") == src_sha1:
+            return data, name
+    return found[0] if found else (None, None)
 
 
 def main():
@@ -310,10 +343,14 @@ def main():
     # src/main.cpp:763-781): same frames as step(), without the per-frame Python and ctypes cost
     # that makes the small configs host-bound.  Pipelined mode 1 and N > 1 keep step().
     host_loop = world == 1 and ref is None and not pipeline
+    # the 8-slot history ring is full before timing whatever --warmup says (>= 8
+    # warm-up frames so the mode-1 temporal filter reads a full ring)
+    ring_fill = max(0, rend.F - args.warmup)
+    warm = args.warmup + ring_fill
     if host_loop:
-        state["frame"] = rend.compute_frames(header, mode, state["frame"], args.warmup, 7000, False)
+        state["frame"] = rend.compute_frames(header, mode, state["frame"], warm, 7000, False)
     else:
-        for k in range(args.warmup):
+        for k in range(warm):
             step(k)
     if gather is not None:
         gather.finish()
@@ -328,22 +365,42 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    host_s = 0.0  # host time inside step() (enqueue): the frame is host-bound if this nears elapsed
+    host_s = 0.0  # host time inside step() (enqueue + back-pressure waits)
+    frame_ev = []  # per-frame completion events (the frame's last stream): median frame interval
     if host_loop:
-        th = time.perf_counter()
-        state["frame"] = rend.compute_frames(header, mode, state["frame"], args.steps, 7000 + args.warmup, False)
-        host_s += time.perf_counter() - th
+        # chunks of the C++ loop, each bracketed by an event: the median chunk's ms per frame
+        nch = min(args.steps, 5)
+        sizes = [args.steps // nch + (1 if i < args.steps % nch else 0) for i in range(nch)]
+        k0 = warm
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        frame_ev.append((ev, 0))
+        for n_ in sizes:
+            th = time.perf_counter()
+            state["frame"] = rend.compute_frames(header, mode, state["frame"], n_, 7000 + k0, False)
+            host_s += time.perf_counter() - th
+            k0 += n_
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream)
+            frame_ev.append((ev, n_))
     else:
-        for k in range(args.warmup, args.warmup + args.steps):
+        for k in range(warm, warm + args.steps):
             th = time.perf_counter()
             step(k)
             host_s += time.perf_counter() - th
+            if world == 1:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(streams["out"])
+                frame_ev.append((ev, 1))
     if gather is not None:
         gather.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    host_wait_ms, host_waits = rend.host_stats()
+    intervals = [frame_ev[i][0].elapsed_time(frame_ev[i + 1][0]) / frame_ev[i + 1][1]
+                 for i in range(len(frame_ev) - 1)] if frame_ev else []
     rend.enable_timing(False)
     progs = {1: [1, 2], 2: [3], 3: [4], 4: [5]}[mode]
     kstats = {p: rend.kernel_stats(p) for p in progs}
@@ -358,9 +415,9 @@ def main():
     rend.enable_timing(True)
     rend.reset_stats()
     if host_loop:  # events recorded inside the C++ loop: no host submission gap in the bracket
-        state["frame"] = rend.compute_frames(header, mode, state["frame"], 4, 7000 + args.warmup, False)
+        state["frame"] = rend.compute_frames(header, mode, state["frame"], 4, 7000 + warm, False)
     else:
-        for k in range(args.warmup, args.warmup + 2):
+        for k in range(warm, warm + 2):
             step(k)
     if gather is not None:
         gather.finish()
@@ -369,7 +426,7 @@ def main():
     rend.enable_counters(True)
     rend.read_counters(reset=True)
     ncount = 2
-    for k in range(args.warmup, args.warmup + ncount):
+    for k in range(warm, warm + ncount):
         step(k)
     if gather is not None:
         gather.finish()
@@ -405,7 +462,8 @@ def main():
         sustained = FLOP_PER_TEST * tests / (elapsed / args.steps) / 1e12
         band_px = (r1 - r0 + (2 if mode in (1, 2) and world > 1 else 0)) * W
         hbm_alg = BYTES_PER_PIXEL[dom] * band_px / (avg_ms * 1e-3) / 1e9
-        traffic_data, traffic_src = load_traffic(args.config)
+        binfo = build_info()
+        traffic_data, traffic_src = load_traffic(args.config, binfo.get("src_sha1"))
         roof = {
             "bound": "valu",
             "achieved": round(tflops, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
@@ -427,11 +485,18 @@ def main():
                     "frac": round(hbm_alg / PEAK_HBM_GBPS, 6),
                     "bytes_per_launch": BYTES_PER_PIXEL[dom] * band_px},
             "traffic_source": traffic_src,
+            # the PMC run's library build vs this one: equal source hashes = measured on this kernel code
+            "traffic_src_sha1": traffic_data.get("src_sha1") if traffic_data else None,
+            "traffic_on_this_build": bool(traffic_data and traffic_data.get("src_sha1") == binfo.get("src_sha1")),
         }
         out = {
             "metric": "Mrays/s + ms/frame at 3840x2160, 16 AO samples, 64 spheres; 1/2/4/8 GPU",
             "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "warmup": args.warmup, "ring_fill_frames": ring_fill, "ms_per_step": round(ms, 4),
+            "ms_per_step_median": round(float(np.median(intervals)), 4) if intervals else None,
+            "ms_per_step_median_of": ("per-frame completion intervals (events on the output stream)" if not host_loop
+                                      else f"{len(intervals)} chunks of the C++ frame loop") if intervals else None,
+            "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": desc, "width": W, "height": H, "spheres": S, "spp": spp, "mode": mode,
                        "max_depth": 20, "strips": plan.bounds,
@@ -440,7 +505,11 @@ def main():
                           if pipeline else "")
                        + (", frame loop in C++ (rt_compute_frames)" if host_loop else "")},
             "roofline": roof,
-            "host_ms_per_step": round(float(host_max.item()) / args.steps * 1e3, 4),
+            # host time per frame inside the frame calls = enqueue + waits for a free staging
+            # buffer (back-pressure: the host runs up to 8 uploads ahead of the GPU)
+            "host_enqueue_ms_per_step": round(max(0.0, host_s * 1e3 - host_wait_ms) / args.steps, 4),
+            "host_backpressure_ms_per_step": round(host_wait_ms / args.steps, 4),
+            "build": binfo,
         }
         if balance_info is not None:
             sm = strip_ms.cpu().tolist()

@@ -204,6 +204,10 @@ int rt_enable_timing(rt_ctx* ctx, int on);
 /* Sum of event-measured durations of `program`'s kernel since the last reset. */
 int rt_kernel_stats(rt_ctx* ctx, int program, int* launches, double* total_ms);
 int rt_reset_stats(rt_ctx* ctx);
+/* Host time (ms) the context's uploads spent waiting for a free pinned staging buffer — back-
+ * pressure when the host runs more than 8 uploads ahead of the GPU — and how many waits,
+ * since the last rt_reset_stats.  Host time per frame minus this is the enqueue cost. */
+int rt_host_stats(rt_ctx* ctx, double* wait_ms, long long* waits);
 /* Work counters (a separate, un-timed instrumentation mode).  on = bit 0: totals, bit 1:
  * per-row counts.  Totals, added by every trace launch: [0] primary samples, [1] closest-hit
  * segments (one scene loop each), [2] shadow rays, [3] ray-shape tests = ([1] + [2]) *

@@ -15,6 +15,10 @@ import numpy as np
 
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "build" / "librt_oracle.so"
+# the same C source built for Zen with AVX-512 (make oracle: -march=znver3 + AVX-512; gcc 11
+# has no znver4): the CPU baseline's build for the GPU box's AMD EPYC host cores (BASELINE.md:
+# the CPU reference built for its own host); tests use the portable x86-64-v3 build
+NATIVE_PATH = HERE / "build" / "librt_oracle_zen.so"
 
 AOP_COMPUTE, AOP_POSTPROCESSING, AO_COMPUTE, P_COMPUTE, H_COMPUTE = 1, 2, 3, 4, 5
 
@@ -29,6 +33,26 @@ _lib = None
 def build():
     """Compile the oracle with gcc (Makefile target `oracle`)."""
     subprocess.run(["make", "-s", "oracle"], cwd=HERE.parent, check=True)
+
+
+def select_native() -> bool:
+    """Use the Zen AVX-512 build for this process when the host is an AVX-512 AMD CPU (before the
+    first load; CPU-baseline timing only)."""
+    global LIB_PATH
+    if _lib is not None or not NATIVE_PATH.exists():
+        return False
+    try:
+        info = Path("/proc/cpuinfo").read_text()
+    except OSError:
+        return False
+    if "AuthenticAMD" in info and " avx512f" in info and " avx512vl" in info:
+        LIB_PATH = NATIVE_PATH
+        return True
+    return False
+
+
+def lib_name() -> str:
+    return LIB_PATH.name
 
 
 def load():

@@ -579,26 +579,28 @@ int rto_run_program_window(float* ssbo, const rto_dims* d, int program, int fram
     float* snap = (float*)malloc(slot * sizeof(float));
     if (!snap) return -1;
     memcpy(snap, c.pix + (size_t)frame * slot, slot * sizeof(float));
+    /* every pixel is independent: threads share the window's pixels (chunks of 64), not rows,
+       so a thin band still uses every thread */
+    const long long w = x1 - x0, npx = w * (long long)(y1 - y0);
 #ifdef _OPENMP
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nt)
 #endif
-    for (int y = y0; y < y1; y++)
-      for (int x = x0; x < x1; x++) post_main(&c, snap, x, y, image);
+    for (long long i = 0; i < npx; i++) post_main(&c, snap, x0 + (int)(i % w), y0 + (int)(i / w), image);
     free(snap);
     return 0;
   }
+  const long long w = x1 - x0, npx = w * (long long)(y1 - y0);
 #ifdef _OPENMP
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nt)
 #endif
-  for (int y = y0; y < y1; y++) {
-    for (int x = x0; x < x1; x++) {
-      switch (program) {
-        case RTO_P_COMPUTE: p_main(&c, x, y, image); break;
-        case RTO_H_COMPUTE: h_main(&c, x, y, image); break;
-        case RTO_AO_COMPUTE: ao_main(&c, x, y, image, 1); break;
-        case RTO_AOP_COMPUTE: ao_main(&c, x, y, image, 0); break;
-        default: break;
-      }
+  for (long long i = 0; i < npx; i++) {
+    const int x = x0 + (int)(i % w), y = y0 + (int)(i / w);
+    switch (program) {
+      case RTO_P_COMPUTE: p_main(&c, x, y, image); break;
+      case RTO_H_COMPUTE: h_main(&c, x, y, image); break;
+      case RTO_AO_COMPUTE: ao_main(&c, x, y, image, 1); break;
+      case RTO_AOP_COMPUTE: ao_main(&c, x, y, image, 0); break;
+      default: break;
     }
   }
   return 0;

@@ -84,6 +84,7 @@ SIGNATURES = {
     "rt_enable_timing": (C.c_int, [_ctx, C.c_int]),
     "rt_kernel_stats": (C.c_int, [_ctx, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]),
     "rt_reset_stats": (C.c_int, [_ctx]),
+    "rt_host_stats": (C.c_int, [_ctx, C.POINTER(C.c_double), C.POINTER(C.c_longlong)]),
     "rt_enable_counters": (C.c_int, [_ctx, C.c_int]),
     "rt_read_counters": (C.c_int, [_ctx, C.POINTER(C.c_uint64), C.c_int]),
     "rt_read_row_counters": (C.c_int, [_ctx, C.POINTER(C.c_uint64), C.c_int]),

@@ -66,12 +66,15 @@ __device__ __forceinline__ float pow500(float x) {
   return ((((x256 * x128) * x64) * x32) * x16) * x4;
 }
 
-// 16x16 pixel tile per 256-lane block, 8x8 per wave (ray coherence inside a wave).
-__device__ __forceinline__ void tile_xy(int& x, int& y, int row0) {
+// 8x8 pixels per wave (ray coherence inside a wave), BWX x BWY waves per block (16x16 pixels
+// per 256-lane block by default); block tile (bx, by) of the trace rows.
+template <int BWX = 2, int BWY = 2>
+__device__ __forceinline__ void tile_xy(int& x, int& y, int row0, int bx, int by) {
   int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-  y = row0 + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+  x = bx * 8 * BWX + (wave % BWX) * 8 + (lane & 7);
+  y = row0 + by * 8 * BWY + (wave / BWX) * 8 + (lane >> 3);
 }
+__device__ __forceinline__ void tile_xy(int& x, int& y, int row0) { tile_xy<2, 2>(x, y, row0, blockIdx.x, blockIdx.y); }
 
 // Work counters for the algorithmic-FLOP roofline (only when P.counters is set).  Called by
 // every lane of a wave with the wave converged; one atomic per counter per wave.
@@ -346,7 +349,8 @@ __device__ __forceinline__ unsigned long long plane_cone_mask(const FrameParams&
 // word the wave culls the spheres lane-parallel, then tests the survivors in ascending index
 // order, reading them on the scalar path (wave-uniform index).  PL: then the planes the cone
 // does not exclude.  Same result as closest_hit.  Must be called by every lane of the wave.
-template <bool PL>
+// SKIP (timing ablation): cull only, no tests.
+template <bool PL, bool SKIP = false>
 __device__ __forceinline__ int closest_hit_cone(const FrameParams& P, const float4* __restrict__ geo, int nobj,
                                                 const ConeF& cone, f3 cam, f3 dir, float thr, float& t_out) {
   float t = -1.0f;
@@ -356,7 +360,7 @@ __device__ __forceinline__ int closest_hit_cone(const FrameParams& P, const floa
     const int i = w + lane;
     const bool keep = i < nobj && !cone_misses_f(cone, geo[i], cam.x, cam.y, cam.z);
     unsigned long long m = uniform_mask(__ballot(keep));
-    while (m) {
+    while (m && !SKIP) {
       const int k = w + __builtin_ctzll(m);
       m &= m - 1;
       sphere_candidate(cam, dir, geo[k], k, thr, t, ind);
@@ -367,10 +371,11 @@ __device__ __forceinline__ int closest_hit_cone(const FrameParams& P, const floa
   return ind;
 }
 
-// The cone of the camera rays through this wave's 8x8 pixel tile (tile_xy).
-__device__ __forceinline__ ConeF wave_tile_cone(const FrameParams& P) {
+// The cone of the camera rays through this wave's 8x8 pixel tile (tile_xy of tile (bx, by)).
+template <int BWX = 2, int BWY = 2>
+__device__ __forceinline__ ConeF wave_tile_cone(const FrameParams& P, int bx, int by) {
   const int wave = threadIdx.x >> 6;
-  const int x0 = blockIdx.x * 16 + (wave & 1) * 8, y0 = P.trace_row0 + blockIdx.y * 16 + (wave >> 1) * 8;
+  const int x0 = bx * 8 * BWX + (wave % BWX) * 8, y0 = P.trace_row0 + by * 8 * BWY + (wave / BWX) * 8;
   return pool_cone_f(P, x0, x0 + 7, y0, y0 + 7);
 }
 
@@ -409,18 +414,14 @@ __device__ __forceinline__ bool shadow_lit_cone(const FrameParams& P, const floa
     }
     return lit;
   }
-  // cone at the light over the directions -l of the lanes that need a shadow ray
-  float sx = need ? -l.x : 0.0f, sy = need ? -l.y : 0.0f, sz = need ? -l.z : 0.0f;
-  for (int o = 32; o > 0; o >>= 1) {
-    sx += __shfl_xor(sx, o);
-    sy += __shfl_xor(sy, o);
-    sz += __shfl_xor(sz, o);
-  }
+  // cone at the light over the directions -l of the lanes that need a shadow ray (DPP
+  // reductions; the cone only has to contain every lane's direction, whatever the sum order)
+  const float sx = wave_sum_f(need ? -l.x : 0.0f), sy = wave_sum_f(need ? -l.y : 0.0f),
+              sz = wave_sum_f(need ? -l.z : 0.0f);
   const float il = __builtin_amdgcn_rsqf(sx * sx + sy * sy + sz * sz);
   ConeF cone;
   cone.ax = sx * il; cone.ay = sy * il; cone.az = sz * il;
-  float cd = need ? -(cone.ax * l.x + cone.ay * l.y + cone.az * l.z) : 1.0f;
-  for (int o = 32; o > 0; o >>= 1) cd = fminf(cd, __shfl_xor(cd, o));
+  float cd = wave_min_f(need ? -(cone.ax * l.x + cone.ay * l.y + cone.az * l.z) : 1.0f);
   cd = fminf(fmaxf(cd - 2e-5f, -1.0f), 1.0f);
   cone.ct = cd;
   cone.st = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - cd * cd));
@@ -469,26 +470,22 @@ __device__ __forceinline__ bool shadow_lit_sph(const FrameParams& P, const float
 // their shadow rays are cone-culled, and PL adds the scene's planes (plane table, tested after
 // the spheres).  !ALLSPH (A/B builds only): the whole shape table staged in LDS, every shape
 // tested through eval_ray's id dispatch, no culling.
-template <bool ALLSPH, bool PL = false>
-__global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
-  extern __shared__ float4 lds[];
-  if (!ALLSPH) {
-    stage_shapes(P, lds);
-    __syncthreads();
-  }
+template <bool ALLSPH, bool PL, bool LT, int BWX = 2, int BWY = 2>
+__device__ __forceinline__ void phong_tile(const FrameParams& P, const float4* lds, int bx, int by) {
   const int n = P.nobj;
-  const float4* tab = ALLSPH ? P.shapes : lds;  // geo | geo2 | col
-  const float4* geo = ALLSPH ? P.sph : lds;     // what the sphere tests read
-  const float4 *geo2 = tab + (ALLSPH ? P.S : n), *col = tab + 2 * (ALLSPH ? P.S : n);
+  const float4* tab = (ALLSPH && !LT) ? P.shapes : lds;                       // geo | geo2 | col
+  const float4* geo = (ALLSPH && !LT) ? P.sph : (ALLSPH ? lds + 4 * n : lds);  // what the sphere tests read
+  const int stride = (ALLSPH && !LT) ? P.S : n;
+  const float4 *geo2 = tab + stride, *col = tab + 2 * stride;
   int x, y;
-  tile_xy(x, y, P.trace_row0);
+  tile_xy<BWX, BWY>(x, y, P.trace_row0, bx, by);
   const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
   const f3 cam = mk(P.cx, P.cy, P.cz), light = mk(P.Lx, P.Ly, P.Lz);
   const f3 dir = primary_dir(P, div_rn_by((float)x, P.fW, P.inv_W), div_rn_by((float)y, P.fH, P.inv_H));
   float t;
   int ind;
   if (ALLSPH) {
-    const ConeF cone = wave_tile_cone(P);
+    const ConeF cone = wave_tile_cone<BWX, BWY>(P, bx, by);
     ind = closest_hit_cone<PL>(P, geo, n, cone, cam, dir, 0.0f, t);
   } else {
     ind = closest_hit<ALLSPH>(geo, geo2, n, cam, dir, 0.0f, t);
@@ -520,52 +517,129 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
   store_color(P, x, y, gamma_out(0.0f + r, 0.0f + g, 0.0f + b));
 }
 
+// LT (ALLSPH, scenes of at most kTabLdsMax objects): the block stages the shape tables and the
+// sphere table in LDS once ([4][n] + [n] float4), so the culls, the survivors' tests, the shadow
+// rays and the shading read LDS instead of making dependent global round trips, whose latency
+// the few resident waves of these short kernels do not hide.
+constexpr int kTabLdsMax = 128;
+__device__ __forceinline__ void stage_tables(const FrameParams& P, float4* lds) {
+  const int n = P.nobj;
+  stage_shapes(P, lds);
+  for (int k = threadIdx.x; k < n; k += blockDim.x) lds[4 * n + k] = P.sph[k];
+}
+
+template <bool ALLSPH, bool PL = false, bool LT = false>
+__global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
+  extern __shared__ float4 lds[];
+  if (!ALLSPH || LT) {
+    if (LT) stage_tables(P, lds);
+    else stage_shapes(P, lds);
+    __syncthreads();
+  }
+  phong_tile<ALLSPH, PL, LT>(P, lds, blockIdx.x, blockIdx.y);
+}
+
 // ---------------------------------------------------------------------------------------
 // mode 4 — h_compute.glsl:186-321
 // ---------------------------------------------------------------------------------------
-template <bool ALLSPH, bool PL = false>
-__global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
-  extern __shared__ float4 lds[];  // !ALLSPH: LDS table (see phong_kernel)
-  if (!ALLSPH) {
-    stage_shapes(P, lds);
-    __syncthreads();
+// Mirror bounces (segments >= 1) of the live paths of a wave, one segment per round.  Few
+// paths bounce (~3% of the pixels at config (b)), so a round usually has a handful of live
+// lanes; then each live path gets a group of G = 64 / 2^ceil(log2 L) lanes: lane p of the group
+// tests spheres p, p+G, ... and the group merges the partial closest hits (minimum t, lowest
+// index on ties: exactly the ascending scan of h_compute.glsl:121-139), and likewise splits the
+// segment's shadow ray ("some occluder exists" is order-free, p_compute.glsl:145-166).  With
+// more than 32 live paths every lane traces its own.  Returns (for the owner lanes) t, ind, lit.
+// Must be called by every lane of the wave; perm: this wave's 64-int LDS slice.
+template <bool PL>
+__device__ __forceinline__ void bounce_round(const FrameParams& P, const float4* __restrict__ geo, int n, f3 light,
+                                             bool live, f3 pos, f3 dir, int* perm, float& t_out, int& ind_out,
+                                             bool& lit_out) {
+  const unsigned long long lm = __ballot(live);
+  const int L = __popcll(lm);
+  const int lane = threadIdx.x & 63;
+  if (L > 32) {
+    float t = -1.0f;
+    int ind = -1;
+    bool lit = true;
+    if (live) {
+      ind = closest_hit_pf(geo, n, pos, dir, 0.001f, t);
+      if (PL) plane_pass(P, pos, dir, 0.001f, t, ind);
+      if (ind != -1) lit = shadow_lit_sph<PL>(P, geo, n, light, pos + t * dir);
+    }
+    t_out = t;
+    ind_out = ind;
+    lit_out = lit;
+    return;
   }
-  const int n = P.nobj;
-  const float4* tab = ALLSPH ? P.shapes : lds;
-  const float4* geo = ALLSPH ? P.sph : lds;
-  const int stride = ALLSPH ? P.S : n;
+  int c = 0;
+  while ((1 << c) < L) ++c;
+  const int G = 64 >> c;  // the largest power of 2 with G * L <= 64
+  const int rk = __builtin_amdgcn_mbcnt_hi((unsigned)(lm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)lm, 0u));
+  if (live) perm[rk] = lane;
+  __builtin_amdgcn_wave_barrier();
+  const int g = lane / G, pl = lane - g * G;
+  const bool act = g < L;
+  const int owner = act ? perm[g] : lane;
+  __builtin_amdgcn_wave_barrier();
+  const f3 o = mk(__shfl(pos.x, owner), __shfl(pos.y, owner), __shfl(pos.z, owner));
+  const f3 d = mk(__shfl(dir.x, owner), __shfl(dir.y, owner), __shfl(dir.z, owner));
+  float t = -1.0f;
+  int ind = -1;
+  if (act)
+    for (int i = pl; i < n; i += G) sphere_candidate(o, d, geo[i], i, 0.001f, t, ind);
+  for (int m = 1; m < G; m <<= 1) {  // every lane of the group ends with the group's result
+    const float tb = __shfl_xor(t, m);
+    const int ib = __shfl_xor(ind, m);
+    const bool take = ib >= 0 && (ind < 0 || tb < t || (tb == t && ib < ind));
+    t = take ? tb : t;
+    ind = take ? ib : ind;
+  }
+  if (PL && act) plane_pass(P, o, d, 0.001f, t, ind);  // same planes, same result on every group lane
+  // the segment's shadow ray, split the same way (the owner's hit point, same float ops)
+  bool occ = false;
+  if (act && ind != -1) {
+    const f3 curr = o + t * d;
+    const f3 lv = light - curr;
+    const f3 l = normalize(lv);
+    const float len = sqrtf(dot(lv, lv));
+    const f3 np = curr + 0.01f * l;
+    const double dlen = (double)len;
+    if (PL)
+      for (int k = pl; k < P.nplanes && !occ; k += G)
+        occ = shadow_occludes(plane_eval(np, l, P.planes[2 * k], P.planes[2 * k + 1]), l, dlen);
+    for (int i = pl; i < n && !occ; i += G) occ = shadow_occludes(sphere_eval_shadow(np, l, geo[i]), l, dlen);
+  }
+  unsigned oc = occ ? 1u : 0u;
+  for (int m = 1; m < G; m <<= 1) oc |= (unsigned)__shfl_xor((int)oc, m);
+  const int src = live ? rk * G : lane;
+  t_out = __shfl(t, src);
+  ind_out = __shfl(ind, src);
+  lit_out = __shfl((int)oc, src) == 0;
+}
+
+// ABL (A/B builds only, timing ablations): 1 = no shadow rays, 2 = no scene tests at all,
+// 3 = primary cull only, 5 = no bounce segments, 6 = bounces without the split rounds
+template <bool ALLSPH, bool PL, bool LT, int ABL = 0, int BWX = 2, int BWY = 2>
+__device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* lds, int* perm, int bx, int by) {
+  const int n = P.nobj;  // !ALLSPH or LT: LDS tables (see phong_kernel)
+  const float4* tab = (ALLSPH && !LT) ? P.shapes : lds;
+  const float4* geo = (ALLSPH && !LT) ? P.sph : (ALLSPH ? lds + 4 * n : lds);
+  const int stride = (ALLSPH && !LT) ? P.S : n;
   const float4 *geo2 = tab + stride, *col = tab + 2 * stride, *aux = tab + 3 * stride;
   int x, y;
-  tile_xy(x, y, P.trace_row0);
+  tile_xy<BWX, BWY>(x, y, P.trace_row0, bx, by);
   const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
   const f3 light = mk(P.Lx, P.Ly, P.Lz);
+  const unsigned long long tstart = ABL == 7 ? __builtin_amdgcn_s_memrealtime() : 0;
   f3 pos = mk(P.cx, P.cy, P.cz);
   f3 dir = primary_dir(P, div_rn_by((float)x, P.fW, P.inv_W), div_rn_by((float)y, P.fH, P.inv_H));
   float arefl = 0.0f;          // array[2].w
   float rr = 0, rg = 0, rb = 0;  // result_color.rgb
   float c = 0.0f;
   unsigned nseg = 0, nshadow = 0;
-  float t0 = -1.0f;
-  int ind0 = -1;
-  bool lit0 = true;
-  if (ALLSPH) {  // the camera rays of the wave's 8x8 tile and their shadow rays, cone-culled
-    const ConeF cone = wave_tile_cone(P);
-    ind0 = closest_hit_cone<PL>(P, geo, n, cone, pos, dir, 0.001f, t0);
-    lit0 = shadow_lit_cone<PL>(P, geo, n, light, pos + t0 * dir, active && ind0 != -1);  // every lane takes part
-  }
-  for (int seg = 0; active && seg < P.D; ++seg) {  // helper depth D, D-1, ..., 1
-    // ---- hybrid_helper ----
-    float t;
-    int ind;
-    if (ALLSPH && seg == 0) {  // camera rays: culled before the loop, with the whole wave
-      t = t0;
-      ind = ind0;
-    } else if (ALLSPH) {
-      ind = closest_hit_pf(geo, n, pos, dir, 0.001f, t);
-      if (PL) plane_pass(P, pos, dir, 0.001f, t, ind);
-    } else {
-      ind = closest_hit<ALLSPH>(geo, geo2, n, pos, dir, 0.001f, t);
-    }
+  // hybrid_helper's shading of one segment's hit (or miss) plus hybrid's accumulation
+  // (h_compute.glsl:241-295); returns true when the path stops
+  auto segment = [&](int seg, float t, int ind, bool lit) -> bool {
     ++nseg;
     nshadow += ind == -1 ? 0u : 1u;
     float ar, ag, ab;
@@ -576,9 +650,6 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
     } else {
       float4 att = col[ind];
       f3 curr = pos + t * dir;
-      bool lit = (ALLSPH && seg == 0) ? lit0
-                 : ALLSPH             ? shadow_lit_sph<PL>(P, geo, n, light, curr)
-                                      : shadow_lit<ALLSPH>(geo, geo2, n, light, curr);
       int id = (ALLSPH && !PL) ? SHAPE_SPHERE : __float_as_int(geo2[ind].w);
       f3 nn = shape_normal(tab[ind], id, curr);
       if (lit) {
@@ -601,7 +672,6 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
         arefl = refl;
       }
     }
-    // ---- hybrid (h_compute.glsl:279-295) ----
     if (seg == 0) {
       c = arefl;
       rr = ar; rg = ag; rb = ab;
@@ -612,10 +682,65 @@ __global__ __launch_bounds__(kBlock) void hybrid_kernel(FrameParams P) {
       rb = (rb + c * ab) / den;
       c = c * arefl;
     }
-    if (stop) break;
+    return stop;
+  };
+  if (ALLSPH) {
+    // segment 0: the camera rays of the wave's 8x8 tile and their shadow rays, cone-culled
+    float t0 = -1.0f;
+    int ind0 = -1;
+    bool lit0 = true;
+    const ConeF cone = wave_tile_cone<BWX, BWY>(P, bx, by);
+    if (ABL != 2) ind0 = closest_hit_cone<PL, ABL == 3>(P, geo, n, cone, pos, dir, 0.001f, t0);
+    if (ABL == 0 || ABL >= 4) lit0 = shadow_lit_cone<PL>(P, geo, n, light, pos + t0 * dir, active && ind0 != -1);  // every lane takes part
+    bool live = active && !segment(0, t0, ind0, lit0);
+    // segments 1 .. D-1: bounce rounds with the whole wave
+    for (int seg = 1; seg < (ABL == 5 ? 1 : P.D); ++seg) {
+      if (__ballot(live) == 0) break;
+      float t;
+      int ind;
+      bool lit = true;
+      if (ABL == 6) {
+        if (live) {
+          ind = closest_hit_pf(geo, n, pos, dir, 0.001f, t);
+          if (PL) plane_pass(P, pos, dir, 0.001f, t, ind);
+          if (ind != -1) lit = shadow_lit_sph<PL>(P, geo, n, light, pos + t * dir);
+        }
+      } else {
+        bounce_round<PL>(P, geo, n, light, live, pos, dir, perm, t, ind, lit);
+      }
+      if (live) live = !segment(seg, t, ind, lit);
+    }
+  } else {
+    for (int seg = 0; active && seg < P.D; ++seg) {  // helper depth D, D-1, ..., 1
+      float t;
+      const int ind = closest_hit<ALLSPH>(geo, geo2, n, pos, dir, 0.001f, t);
+      const bool lit = ind == -1 || shadow_lit<ALLSPH>(geo, geo2, n, light, pos + t * dir);
+      if (segment(seg, t, ind, lit)) break;
+    }
   }
   count_work(P, active, y, nseg, nshadow);
   if (active) store_color(P, x, y, gamma_out(0.0f + rr, 0.0f + rg, 0.0f + rb));
+  if (ABL == 7) {  // per-wave timeline (tools/explore/wave_timeline.py): lane 0's pixel slot holds
+    // (start, end) of the wave's s_memtime and its longest path in segments
+    const unsigned mx = wave_max(active ? nseg : 0u);
+    const unsigned long long tend = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0 && active)
+      P.out_pix[(size_t)(y - P.band_row0) * P.W + x] =
+          make_float4(__uint_as_float((unsigned)tstart), __uint_as_float((unsigned)tend), __uint_as_float(mx),
+                      __uint_as_float((unsigned)(tstart >> 32)));
+  }
+}
+
+template <bool ALLSPH, bool PL = false, bool LT = false, int ABL = 0, int BWX = 2, int BWY = 2>
+__global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(FrameParams P) {
+  extern __shared__ float4 lds[];
+  __shared__ int hperm[64 * BWX * BWY];  // bounce_round's live-rank -> lane map, a slice per wave
+  if (!ALLSPH || LT) {
+    if (LT) stage_tables(P, lds);
+    else stage_shapes(P, lds);
+    __syncthreads();
+  }
+  hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x, blockIdx.y);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1799,6 +1924,7 @@ __global__ void selftest_kernel(int fn, const float* __restrict__ in, float* __r
 }
 
 size_t shapes_lds_bytes(const FrameParams& p) { return (size_t)4 * p.nobj * sizeof(float4); }
+size_t tab_lds_bytes(const FrameParams& p) { return (size_t)5 * (p.nobj > 0 ? p.nobj : 1) * sizeof(float4); }
 
 }  // namespace
 
@@ -1847,7 +1973,15 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
       hipLaunchKernelGGL((ao_kernel<false, 0>), dim3((unsigned)grid), dim3(block), sh, stream, q, q.shapes);
     return true;
   }
-  if (variant == 7 || p.nplanes > 0) return false;  // production
+  if (variant == 7 || (p.nplanes > 0 && variant != 93)) return false;  // production
+  if (variant == 93 && p.nplanes > 0) {  // section clocks of the production plane kernel
+    const size_t pl_sh = (size_t)batch_lds(p.spp, kPool, tl ? p.nobj : 0).total;
+    if (tl && p.spp == 16)
+      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true, 16, true, true, true>), g, b, pl_sh, stream, q, q.sph);
+    else
+      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, false, true, 0, false, true, true>), g, b, pl_sh, stream, q, q.sph);
+    return true;
+  }
   const size_t psh = (size_t)batch_lds(p.spp, kPool, (variant == 9 || variant == 27 || variant == 93) && tl ? p.nobj : 0).total;
   if (variant == 9 && p.spp == 16 && tl)  // 7 without the per-ray first-bounce pre-test
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 16, false, false>), g, b, psh, stream, q, q.sph);
@@ -1921,6 +2055,30 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
   }
   dim3 grid((p.W + 15) / 16, (p.trace_rows + 15) / 16);
 #if RTRT_AB
+  if (const char* ea = getenv("RTRT_HY_ABL"); ea && program == K_HYBRID && !pl && atoi(ea) > 0) {
+    const int a = atoi(ea);
+    const size_t lt = tab_lds_bytes(p);
+    if (a == 1) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 1>), grid, dim3(kBlock), lt, stream, q);
+    else if (a == 3) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 3>), grid, dim3(kBlock), lt, stream, q);
+    else if (a == 5) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 5>), grid, dim3(kBlock), lt, stream, q);
+    else if (a == 6) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 6>), grid, dim3(kBlock), lt, stream, q);
+    else if (a == 7) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 7>), grid, dim3(kBlock), lt, stream, q);
+    else if (a == 8) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 7>), grid, dim3(kBlock), 0, stream, q);
+    else hipLaunchKernelGGL((hybrid_kernel<true, false, true, 2>), grid, dim3(kBlock), lt, stream, q);
+    return hipGetLastError();
+  }
+  if (const char* eb = getenv("RTRT_HY_BLK"); eb && program == K_HYBRID && !pl) {  // block shape A/B
+    const int k = atoi(eb);
+    auto gr = [&](int bwx, int bwy) { return dim3((p.W + 8 * bwx - 1) / (8 * bwx), (p.trace_rows + 8 * bwy - 1) / (8 * bwy)); };
+    const size_t lt = tab_lds_bytes(p);
+    if (k == 11) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 1, 1>), gr(1, 1), dim3(64), lt, stream, q);
+    else if (k == 21) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 2, 1>), gr(2, 1), dim3(128), lt, stream, q);
+    else if (k == 41) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 4, 1>), gr(4, 1), dim3(256), lt, stream, q);
+    else if (k == 42) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 4, 2>), gr(4, 2), dim3(512), lt, stream, q);
+    else if (k == 44) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 4, 4>), gr(4, 4), dim3(1024), lt, stream, q);
+    else hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 2, 2>), grid, dim3(kBlock), lt, stream, q);
+    return hipGetLastError();
+  }
   if (ab_general() && (program == K_PHONG || program == K_HYBRID)) {
     const size_t lds = shapes_lds_bytes(p);
     if (program == K_PHONG) hipLaunchKernelGGL((phong_kernel<false>), grid, dim3(kBlock), lds, stream, q);
@@ -1928,14 +2086,21 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
     return hipGetLastError();
   }
 #endif
+  // scenes of at most kTabLdsMax objects: the tables staged in LDS per wave (LT)
+  const bool lt = p.nobj <= kTabLdsMax;
+  const size_t ltb = lt ? tab_lds_bytes(p) : 0;
   switch (program) {
     case K_PHONG:
-      if (pl) hipLaunchKernelGGL((phong_kernel<true, true>), grid, dim3(kBlock), 0, stream, q);
-      else hipLaunchKernelGGL((phong_kernel<true, false>), grid, dim3(kBlock), 0, stream, q);
+      if (pl && lt) hipLaunchKernelGGL((phong_kernel<true, true, true>), grid, dim3(kBlock), ltb, stream, q);
+      else if (pl) hipLaunchKernelGGL((phong_kernel<true, true, false>), grid, dim3(kBlock), 0, stream, q);
+      else if (lt) hipLaunchKernelGGL((phong_kernel<true, false, true>), grid, dim3(kBlock), ltb, stream, q);
+      else hipLaunchKernelGGL((phong_kernel<true, false, false>), grid, dim3(kBlock), 0, stream, q);
       break;
     case K_HYBRID:
-      if (pl) hipLaunchKernelGGL((hybrid_kernel<true, true>), grid, dim3(kBlock), 0, stream, q);
-      else hipLaunchKernelGGL((hybrid_kernel<true, false>), grid, dim3(kBlock), 0, stream, q);
+      if (pl && lt) hipLaunchKernelGGL((hybrid_kernel<true, true, true>), grid, dim3(kBlock), ltb, stream, q);
+      else if (pl) hipLaunchKernelGGL((hybrid_kernel<true, true, false>), grid, dim3(kBlock), 0, stream, q);
+      else if (lt) hipLaunchKernelGGL((hybrid_kernel<true, false, true>), grid, dim3(kBlock), ltb, stream, q);
+      else hipLaunchKernelGGL((hybrid_kernel<true, false, false>), grid, dim3(kBlock), 0, stream, q);
       break;
     case K_POST:
       hipLaunchKernelGGL(post_kernel, grid, dim3(kBlock), 0, stream, q);

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -103,6 +104,10 @@ struct rt_ctx {
   bool counting = false;
   bool row_counting = false;
   int last_hip = 0;
+  // host time spent waiting for a staging buffer to be free (back-pressure: the host is up to
+  // kStageSlots uploads ahead of the GPU), since the last rt_reset_stats
+  double host_wait_ms = 0.0;
+  long long host_waits = 0;
 };
 
 namespace {
@@ -139,7 +144,16 @@ int staged_copy(rt_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t
   if (bytes == 0) return RT_OK;
   Stage& s = c->stage[c->stage_next];
   c->stage_next = (c->stage_next + 1) % kStageSlots;
-  if (s.used) RT_HIP(c, hipEventSynchronize(s.done));
+  if (s.used) {
+    if (hipEventQuery(s.done) == hipErrorNotReady) {  // the GPU has not consumed it yet: wait
+      const auto t0 = std::chrono::steady_clock::now();
+      RT_HIP(c, hipEventSynchronize(s.done));
+      c->host_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      c->host_waits += 1;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
   if (s.bytes < bytes) {
     if (s.host) RT_HIP(c, hipHostFree(s.host));
     s.host = nullptr;
@@ -863,10 +877,19 @@ int rt_kernel_stats(rt_ctx* c, int program, int* launches, double* total_ms) {
   return RT_OK;
 }
 
+int rt_host_stats(rt_ctx* c, double* wait_ms, long long* waits) {
+  if (!c) return RT_E_INVAL;
+  if (wait_ms) *wait_ms = c->host_wait_ms;
+  if (waits) *waits = c->host_waits;
+  return RT_OK;
+}
+
 int rt_reset_stats(rt_ctx* c) {
   if (!c) return RT_E_INVAL;
   int rc = resolve_timing(c);
   if (rc != RT_OK) return rc;
+  c->host_wait_ms = 0.0;
+  c->host_waits = 0;
   for (int k = 0; k < RT_PROG_COUNT; ++k) {
     c->total_ms[k] = 0.0;
     c->launches[k] = 0;

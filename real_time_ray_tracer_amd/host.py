@@ -305,6 +305,12 @@ class Renderer:
     def reset_stats(self):
         self._c(self._lib.rt_reset_stats(self.ctx), "rt_reset_stats")
 
+    def host_stats(self) -> tuple[float, int]:
+        """(ms, count) of host waits for a free staging buffer since reset_stats (back-pressure)."""
+        ms, n = C.c_double(), C.c_longlong()
+        self._c(self._lib.rt_host_stats(self.ctx, C.byref(ms), C.byref(n)), "rt_host_stats")
+        return ms.value, n.value
+
     def enable_counters(self, totals: bool = True, rows: bool = False):
         self._c(self._lib.rt_enable_counters(self.ctx, int(totals) | (2 if rows else 0)), "rt_enable_counters")
 

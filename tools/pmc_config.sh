@@ -1,0 +1,38 @@
+#!/usr/bin/env bash
+# SQ counter passes for one bench config (one rocprofv3 --pmc run per counter group, no
+# tracing domains), summarised per kernel: tools/pmc_config.sh <tag> <config> [kernel-substring]
+set -euo pipefail
+TAG=$1
+CFG=$2
+KSUB=${3:-kernel}
+REPO=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$REPO/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$REPO"
+export TMPDIR=/tmp
+[ -f "$OUT/counters_list.txt" ] || timeout -k 5 60 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
+G1="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+G2="SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VMEM GRBM_GUI_ACTIVE"
+G3=${PMC_G3:-}
+i=0
+for G in "$G1" "$G2" $([ -n "$G3" ] && echo "G3"); do
+  [ "$G" = "G3" ] && G="$G3"
+  i=$((i+1))
+  timeout -k 10 120 rocprofv3 --pmc $G --output-format csv -d "$OUT/${CFG}_g$i" -o run -- \
+    python3 bench.py --config "$CFG" --steps 10 --warmup 8 --no-cpu-baseline > "$OUT/${CFG}_g$i.log" 2>&1
+done
+python3 - "$OUT" "$CFG" "$KSUB" <<'EOF'
+import csv, glob, os, sys, collections
+out, cfg, ksub = sys.argv[1:4]
+res = collections.defaultdict(lambda: collections.defaultdict(list))
+for d in sorted(glob.glob(os.path.join(out, f"{cfg}_g*"))):
+    if not os.path.isdir(d):
+        continue
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"]
+            if ksub in k:
+                res[k.split("(")[0][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, cs in res.items():
+    print(cfg, k, {c: round(sum(v) / len(v)) for c, v in sorted(cs.items())}, "dispatches", max(len(v) for v in cs.values()))
+EOF

@@ -42,10 +42,16 @@ def collect(d, counter, mode_cfg):
 
 def main():
     fetch_dir, write_dir, cfg, out = sys.argv[1:5]
-    mode_cfg = {"a": 3, "b": 4, "c": 2, "d": 1, "e": 2}[cfg]
+    mode_cfg = {"a": 3, "b": 4, "c": 2, "d": 1, "e": 2, "p": 1, "q": 1, "s1": 1}[cfg]
     fe = collect(fetch_dir, "FETCH_SIZE", mode_cfg)
     wr = collect(write_dir, "WRITE_SIZE", mode_cfg)
     res = {"config": cfg, "units": "bytes per launch (FETCH_SIZE*2*1024 + WRITE_SIZE*1024, median)"}
+    try:  # the library build the counters were taken on (make lib writes BUILD_INFO)
+        info = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                           "real_time_ray_tracer_amd", "BUILD_INFO")))
+        res["src_sha1"], res["commit"] = info.get("src_sha1"), info.get("commit")
+    except Exception:
+        res["src_sha1"] = res["commit"] = None
     for k in sorted(set(fe) | set(wr)):
         f = statistics.median(fe.get(k, [0.0])) * 2 * 1024
         w = statistics.median(wr.get(k, [0.0])) * 1024
