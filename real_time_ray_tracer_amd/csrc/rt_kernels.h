@@ -5,6 +5,7 @@
 namespace rt {
 
 constexpr int kMaxFrames = 16;
+constexpr int kMaxBatch = 32;  // frames per multi-frame Phong/hybrid launch
 constexpr int kCounters = 8;
 constexpr int kCounterSlots = 256;  // per counter, summed by the host
 
@@ -51,6 +52,11 @@ struct FrameParams {
   unsigned long long* counters;
   // optional per-row closest-hit segment counts, indexed by (y - band_row0) (nullptr = off)
   unsigned long long* row_counters;
+  // multi-frame Phong/hybrid launch (mf_n > 0, gridDim.z = mf_n): frame j of the batch renders
+  // into slot (mf_slot0 + j) % F (hist_pix) with light mf_light[j]; only frame mf_n - 1 writes
+  // the image.  The shape table is the same for every frame of the batch.
+  int mf_n, mf_slot0;
+  float4 mf_light[kMaxBatch];
 };
 
 // Device shape table of one header copy, in float4 units from its base (rt_shim fills it):

@@ -126,12 +126,30 @@ __device__ __forceinline__ void count_work(const FrameParams& P, bool active, in
   }
 }
 
-__device__ __forceinline__ void store_color(const FrameParams& P, int x, int y, float4 c) {
-  P.out_pix[(size_t)(y - P.band_row0) * P.W + x] = c;
-  if (P.image) {
+__device__ __forceinline__ void store_color(const FrameParams& P, float4* out_pix, float4* image, int x, int y,
+                                            float4 c) {
+  out_pix[(size_t)(y - P.band_row0) * P.W + x] = c;
+  if (image) {
     int r = y - P.img_row0;
-    if (r >= 0 && r < P.img_rows) P.image[(size_t)r * P.W + x] = c;
+    if (r >= 0 && r < P.img_rows) image[(size_t)r * P.W + x] = c;
   }
+}
+__device__ __forceinline__ void store_color(const FrameParams& P, int x, int y, float4 c) {
+  store_color(P, P.out_pix, P.image, x, y, c);
+}
+
+// The frame a Phong/hybrid block renders: its light, colour slot and image (multi-frame
+// launches: frame blockIdx.z of the batch, see FrameParams::mf_n).
+struct FrameDst {
+  f3 light;
+  float4* out_pix;
+  float4* image;
+};
+__device__ __forceinline__ FrameDst frame_dst(const FrameParams& P) {
+  if (P.mf_n <= 0) return FrameDst{mk(P.Lx, P.Ly, P.Lz), P.out_pix, P.image};
+  const int j = blockIdx.z;
+  const float4 L = P.mf_light[j];
+  return FrameDst{mk(L.x, L.y, L.z), (float4*)P.hist_pix[(P.mf_slot0 + j) % P.F], j == P.mf_n - 1 ? P.image : nullptr};
 }
 
 // ---------------------------------------------------------------------------------------
@@ -471,7 +489,7 @@ __device__ __forceinline__ bool shadow_lit_sph(const FrameParams& P, const float
 // the spheres).  !ALLSPH (A/B builds only): the whole shape table staged in LDS, every shape
 // tested through eval_ray's id dispatch, no culling.
 template <bool ALLSPH, bool PL, bool LT, int BWX = 2, int BWY = 2>
-__device__ __forceinline__ void phong_tile(const FrameParams& P, const float4* lds, int bx, int by) {
+__device__ __forceinline__ void phong_tile(const FrameParams& P, const float4* lds, int bx, int by, const FrameDst& fd) {
   const int n = P.nobj;
   const float4* tab = (ALLSPH && !LT) ? P.shapes : lds;                       // geo | geo2 | col
   const float4* geo = (ALLSPH && !LT) ? P.sph : (ALLSPH ? lds + 4 * n : lds);  // what the sphere tests read
@@ -480,7 +498,7 @@ __device__ __forceinline__ void phong_tile(const FrameParams& P, const float4* l
   int x, y;
   tile_xy<BWX, BWY>(x, y, P.trace_row0, bx, by);
   const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
-  const f3 cam = mk(P.cx, P.cy, P.cz), light = mk(P.Lx, P.Ly, P.Lz);
+  const f3 cam = mk(P.cx, P.cy, P.cz), light = fd.light;
   const f3 dir = primary_dir(P, div_rn_by((float)x, P.fW, P.inv_W), div_rn_by((float)y, P.fH, P.inv_H));
   float t;
   int ind;
@@ -514,7 +532,7 @@ __device__ __forceinline__ void phong_tile(const FrameParams& P, const float4* l
     }
   }
   // result_color = vec4(0) + phong(dir); gamma; w = 0
-  store_color(P, x, y, gamma_out(0.0f + r, 0.0f + g, 0.0f + b));
+  store_color(P, fd.out_pix, fd.image, x, y, gamma_out(0.0f + r, 0.0f + g, 0.0f + b));
 }
 
 // LT (ALLSPH, scenes of at most kTabLdsMax objects): the block stages the shape tables and the
@@ -536,7 +554,7 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
     else stage_shapes(P, lds);
     __syncthreads();
   }
-  phong_tile<ALLSPH, PL, LT>(P, lds, blockIdx.x, blockIdx.y);
+  phong_tile<ALLSPH, PL, LT>(P, lds, blockIdx.x, blockIdx.y, frame_dst(P));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -620,7 +638,8 @@ __device__ __forceinline__ void bounce_round(const FrameParams& P, const float4*
 // ABL (A/B builds only, timing ablations): 1 = no shadow rays, 2 = no scene tests at all,
 // 3 = primary cull only, 5 = no bounce segments, 6 = bounces without the split rounds
 template <bool ALLSPH, bool PL, bool LT, int ABL = 0, int BWX = 2, int BWY = 2>
-__device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* lds, int* perm, int bx, int by) {
+__device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* lds, int* perm, int bx, int by,
+                                            const FrameDst& fd) {
   const int n = P.nobj;  // !ALLSPH or LT: LDS tables (see phong_kernel)
   const float4* tab = (ALLSPH && !LT) ? P.shapes : lds;
   const float4* geo = (ALLSPH && !LT) ? P.sph : (ALLSPH ? lds + 4 * n : lds);
@@ -629,7 +648,7 @@ __device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* 
   int x, y;
   tile_xy<BWX, BWY>(x, y, P.trace_row0, bx, by);
   const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
-  const f3 light = mk(P.Lx, P.Ly, P.Lz);
+  const f3 light = fd.light;
   const unsigned long long tstart = ABL == 7 ? __builtin_amdgcn_s_memrealtime() : 0;
   f3 pos = mk(P.cx, P.cy, P.cz);
   f3 dir = primary_dir(P, div_rn_by((float)x, P.fW, P.inv_W), div_rn_by((float)y, P.fH, P.inv_H));
@@ -719,7 +738,7 @@ __device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* 
     }
   }
   count_work(P, active, y, nseg, nshadow);
-  if (active) store_color(P, x, y, gamma_out(0.0f + rr, 0.0f + rg, 0.0f + rb));
+  if (active) store_color(P, fd.out_pix, fd.image, x, y, gamma_out(0.0f + rr, 0.0f + rg, 0.0f + rb));
   if (ABL == 7) {  // per-wave timeline (tools/explore/wave_timeline.py): lane 0's pixel slot holds
     // (start, end) of the wave's s_memtime and its longest path in segments
     const unsigned mx = wave_max(active ? nseg : 0u);
@@ -740,7 +759,8 @@ __global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(FrameParams P) {
     else stage_shapes(P, lds);
     __syncthreads();
   }
-  hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x, blockIdx.y);
+  hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x, blockIdx.y,
+                                             frame_dst(P));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2053,7 +2073,7 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
     }
     return hipGetLastError();
   }
-  dim3 grid((p.W + 15) / 16, (p.trace_rows + 15) / 16);
+  dim3 grid((p.W + 15) / 16, (p.trace_rows + 15) / 16, p.mf_n > 0 ? p.mf_n : 1);
 #if RTRT_AB
   if (const char* ea = getenv("RTRT_HY_ABL"); ea && program == K_HYBRID && !pl && atoi(ea) > 0) {
     const int a = atoi(ea);

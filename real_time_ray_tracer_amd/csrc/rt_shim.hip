@@ -90,12 +90,19 @@ struct rt_ctx {
   std::vector<float4> table;   // host copy of the device table (rt::table_vec4 float4)
   bool have_header = false;
   int nplanes = 0;             // planes among simple_shapes[0, nobj)
+  float4* d_batch = nullptr;   // rt_compute_frames: a batch of device table copies (one per frame)
+  std::vector<float4> batch_host;
+  std::vector<float> batch_hdr;  // the batch's host headers (camera, light: launch parameters)
   int nobj = 0;
   Stage stage[kStageSlots];
   int stage_next = 0;
   // timing
   bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[RT_PROG_COUNT];  // recorded on the launch stream
+  struct Timed {
+    hipEvent_t e0, e1;
+    int frames;  // frames the launch rendered (multi-frame Phong/hybrid launches: up to kMaxBatch)
+  };
+  std::vector<Timed> pending[RT_PROG_COUNT];  // recorded on the launch stream
   std::vector<hipEvent_t> event_pool;
   double total_ms[RT_PROG_COUNT] = {};
   int launches[RT_PROG_COUNT] = {};
@@ -154,11 +161,13 @@ int staged_copy(rt_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t
       (void)hipGetLastError();
     }
   }
-  if (s.bytes < bytes) {
+  if (s.bytes < bytes) {  // grow to a power of two >= 256 KiB: pinned allocations are slow, keep them rare
     if (s.host) RT_HIP(c, hipHostFree(s.host));
     s.host = nullptr;
-    RT_HIP(c, hipHostMalloc(&s.host, bytes, hipHostMallocDefault));
-    s.bytes = bytes;
+    size_t cap = 256 << 10;
+    while (cap < bytes) cap <<= 1;
+    RT_HIP(c, hipHostMalloc(&s.host, cap, hipHostMallocDefault));
+    s.bytes = cap;
   }
   if (!s.done) RT_HIP(c, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
   std::memcpy(s.host, src, bytes);
@@ -175,8 +184,8 @@ void free_all(rt_ctx* c) {
   }
   for (int k = 0; k < RT_PROG_COUNT; ++k)
     for (auto& pr : c->pending[k]) {
-      (void)hipEventDestroy(pr.first);
-      (void)hipEventDestroy(pr.second);
+      (void)hipEventDestroy(pr.e0);
+      (void)hipEventDestroy(pr.e1);
     }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   for (auto p : c->pix) if (p) (void)hipFree(p);
@@ -187,6 +196,7 @@ void free_all(rt_ctx* c) {
     if (c->d_shapes_buf[k]) (void)hipFree(c->d_shapes_buf[k]);
   }
   if (c->d_counters) (void)hipFree(c->d_counters);
+  if (c->d_batch) (void)hipFree(c->d_batch);
   if (c->d_row_counters) (void)hipFree(c->d_row_counters);
   for (auto e : {c->ev_ao, c->ev_join, c->ev_seq})
     if (e) (void)hipEventDestroy(e);
@@ -292,7 +302,7 @@ int launch(rt_ctx* c, int program, const rt::FrameParams& p, hipStream_t st) {
   if (e != hipSuccess) return hip_fail(c, e);
   if (c->timing) {
     RT_HIP(c, hipEventRecord(e1, st));
-    c->pending[program].emplace_back(e0, e1);
+    c->pending[program].push_back(rt_ctx::Timed{e0, e1, p.mf_n > 0 ? p.mf_n : 1});
   }
   return RT_OK;
 }
@@ -336,6 +346,29 @@ int run_program(rt_ctx* c, int program, int frame) {
     default:
       return RT_E_INVAL;
   }
+}
+
+// Frames slot0, slot0+1, ... (m <= min(kMaxBatch, F), one light each) of a Phong/hybrid program
+// in ONE launch (gridDim.z = m).  The frames of modes 3/4 are independent (each writes its own colour
+// slot; the g-buffer normals/depth are not touched), so they may run concurrently; the image,
+// which the next frame would overwrite, is written by the last frame only.
+int run_program_mf(rt_ctx* c, int program, int slot0, int m, const float4* lights) {
+  if (!c->have_header) return RT_E_STATE;
+  if (program != RT_PROG_P_COMPUTE && program != RT_PROG_H_COMPUTE) return RT_E_INVAL;
+  if (m < 1 || m > rt::kMaxBatch || m > c->cfg.num_frames || slot0 < 0 || slot0 >= c->cfg.num_frames)
+    return RT_E_INVAL;
+  RT_HIP(c, hipSetDevice(c->device));
+  int jr = join(c);
+  if (jr != RT_OK) return jr;
+  rt::FrameParams p;
+  fill_params(c, slot0, p);
+  p.trace_row0 = c->own0;
+  p.trace_rows = c->own_rows;
+  p.out_pix = c->pix[c->pix_slot[slot0]];
+  p.mf_n = m;
+  p.mf_slot0 = slot0;
+  for (int j = 0; j < m; ++j) p.mf_light[j] = lights[j];
+  return launch(c, program, p);
 }
 
 // One pipelined mode-1 frame (see the header comment): AO on the frame's AO stream into free
@@ -405,11 +438,11 @@ int resolve_timing(rt_ctx* c) {
   for (int k = 0; k < RT_PROG_COUNT; ++k) {
     for (auto& pr : c->pending[k]) {
       float ms = 0.0f;
-      RT_HIP(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+      RT_HIP(c, hipEventElapsedTime(&ms, pr.e0, pr.e1));
       c->total_ms[k] += ms;
-      c->launches[k] += 1;
-      c->event_pool.push_back(pr.first);
-      c->event_pool.push_back(pr.second);
+      c->launches[k] += pr.frames;  // per frame: a multi-frame launch counts its frames
+      c->event_pool.push_back(pr.e0);
+      c->event_pool.push_back(pr.e1);
     }
     c->pending[k].clear();
   }
@@ -606,34 +639,36 @@ int rt_synchronize(rt_ctx* c) {
 
 int rt_last_hip_error(rt_ctx* c) { return c ? c->last_hip : 0; }
 
-int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
-  if (!c || !header) return RT_E_INVAL;
+}  // extern "C"
+
+namespace {
+
+// Validate a header and pack it into the device table layout (rt::table_vec4 float4 at `tab`:
+// shape tables, sphere table, plane table, rand_buffer); sets nobj / nplanes.
+int pack_header(rt_ctx* c, const float* h, float4* tab, int& nobj, int& nplanes) {
   const int S = c->cfg.num_shapes, spp = c->cfg.spp;
-  if (bytes != rt_header_bytes(S, spp)) return RT_E_INVAL;
-  const float* h = (const float*)header;
-  float mz = h[RT_HDR_MODE * 4 + 2];
+  const float mz = h[RT_HDR_MODE * 4 + 2];
   if (!(mz >= 0.0f && mz < (float)(S + 1))) return RT_E_INVAL;  // int(mode.z) must be in [0, S]
-  int nobj = (int)mz;
-  std::memcpy(c->header.data(), header, bytes);
+  nobj = (int)mz;
   const float* sh = h + rt_off_shapes() / 4;
   const int Sc = table_stride(c);
   const float qnan = std::numeric_limits<float>::quiet_NaN();
-  float4* sph = c->table.data() + rt::sphere_table(Sc);
-  float4* pln = c->table.data() + rt::plane_table(Sc);
+  float4* sph = tab + rt::sphere_table(Sc);
+  float4* pln = tab + rt::plane_table(Sc);
   int np = 0;
   for (int i = 0; i < S; ++i) {
     const float* s = sh + (size_t)i * 20;
     float idf = s[16 + 3];
     int id = (idf > -2147483648.0f && idf < 2147483648.0f) ? (int)idf : 0;  // int(simple_shapes[i][4].w)
-    c->table[i] = make_float4(s[0], s[1], s[2], s[3]);
+    tab[i] = make_float4(s[0], s[1], s[2], s[3]);
     float4 g2 = make_float4(s[12], s[13], s[14], 0.0f);
     std::memcpy(&g2.w, &id, 4);
-    c->table[(size_t)Sc + i] = g2;
-    c->table[(size_t)2 * Sc + i] = make_float4(s[16], s[17], s[18], s[19]);
-    c->table[(size_t)3 * Sc + i] = make_float4(s[4 + 3], s[12 + 3], 0.0f, 0.0f);
+    tab[(size_t)Sc + i] = g2;
+    tab[(size_t)2 * Sc + i] = make_float4(s[16], s[17], s[18], s[19]);
+    tab[(size_t)3 * Sc + i] = make_float4(s[4 + 3], s[12 + 3], 0.0f, 0.0f);
     // sphere table: the spheres' geometry; every other shape NaN (a NaN discriminant is never
     // accepted: eval_ray's -1 for shapes it does not intersect, p_compute.glsl:121-138)
-    sph[i] = id == RT_SHAPE_SPHERE ? c->table[i] : make_float4(qnan, qnan, qnan, qnan);
+    sph[i] = id == RT_SHAPE_SPHERE ? tab[i] : make_float4(qnan, qnan, qnan, qnan);
     if (i < nobj && id == RT_SHAPE_PLANE) {  // plane table: (normal, bits(index)), (p0, 0)
       float4 a = make_float4(s[0], s[1], s[2], 0.0f);
       std::memcpy(&a.w, &i, 4);
@@ -642,6 +677,28 @@ int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
       ++np;
     }
   }
+  std::memcpy(tab + rt::rand_table(Sc), h + rt_off_rand(S) / 4, (size_t)2 * spp * sizeof(float4));
+  nplanes = np;
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
+  if (!c || !header) return RT_E_INVAL;
+  const int S = c->cfg.num_shapes, spp = c->cfg.spp;
+  if (bytes != rt_header_bytes(S, spp)) return RT_E_INVAL;
+  const float* h = (const float*)header;
+  int nobj = 0, np = 0;
+  {
+    const float mz = h[RT_HDR_MODE * 4 + 2];
+    if (!(mz >= 0.0f && mz < (float)(S + 1))) return RT_E_INVAL;
+  }
+  std::memcpy(c->header.data(), header, bytes);
+  int rc = pack_header(c, h, c->table.data(), nobj, np);
+  if (rc != RT_OK) return rc;
   RT_HIP(c, hipSetDevice(c->device));
   // pipelined: into the header copy of the next frame, on its AO stream (ordered after the AO
   // pass two frames back that read that copy); sequential: in place, on the main stream
@@ -651,8 +708,7 @@ int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
     if (sr != RT_OK) return sr;
   }
   // table + rand_buffer in one upload (per-frame host cost matters for small strips/frames)
-  std::memcpy(c->table.data() + rt::rand_table(Sc), h + rt_off_rand(S) / 4, (size_t)2 * spp * sizeof(float4));
-  int rc = staged_copy(c, c->d_shapes_buf[hc], c->table.data(), c->table.size() * sizeof(float4), ao_stream(c));
+  rc = staged_copy(c, c->d_shapes_buf[hc], c->table.data(), c->table.size() * sizeof(float4), ao_stream(c));
   if (rc != RT_OK) return rc;
   c->d_shapes = c->d_shapes_buf[hc];
   c->d_rb = c->d_rb_buf[hc];
@@ -710,19 +766,100 @@ int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint
   if (frame < 0 || frame >= c->cfg.num_frames) return RT_E_INVAL;
   const int S = c->cfg.num_shapes, spp = c->cfg.spp;
   const size_t bytes = rt_header_bytes(S, spp);
-  for (int k = 0; k < n; ++k) {
+  // the render loop's host update of frame k (src/main.cpp:553-578), then set_mode
+  auto update = [&](int k, int slot) -> int {
     int rc = (mode == RT_MODE_AO_PP || mode == RT_MODE_AO) ? rt_fill_rand_buffer(header, S, spp, rand_seed + (uint64_t)k)
                                                            : rt_moving_light(header, light_movement);
     if (rc != RT_OK) return rc;
     const float mz = header[RT_HDR_MODE * 4 + 2];
     if (!(mz >= 0.0f && mz < (float)(S + 1))) return RT_E_INVAL;
-    rc = rt_set_mode(header, frame, (int)mz);
-    if (rc != RT_OK) return rc;
-    rc = rt_upload_header(c, header, bytes);
-    if (rc != RT_OK) return rc;
-    frame = rt_dispatch(c, mode, frame);
-    if (frame < 0) return frame;
+    return rt_set_mode(header, slot, (int)mz);
+  };
+  if ((mode == RT_MODE_PHONG || mode == RT_MODE_PHONG_REFL) && n >= 2) {
+    // Modes 3/4: the per-frame host update moves only the light (and mode.y), so the shape
+    // table is uploaded once and up to kMaxBatch frames go in one multi-frame launch with their
+    // lights (run_program_mf).  Every frame writes its own colour slot, as frame-by-frame calls
+    // do; the image is written once per launch, by its last frame (the one the caller sees).
+    std::vector<float4> lights(n);
+    std::vector<int> slots(n);
+    int f = frame;
+    for (int k = 0; k < n; ++k) {
+      int rc = update(k, f);
+      if (rc == RT_OK && k == 0) rc = rt_upload_header(c, header, bytes);
+      if (rc != RT_OK) return rc;
+      const float* L = header + 4 * RT_HDR_LIGHT_POS;
+      lights[k] = make_float4(L[0], L[1], L[2], L[3]);
+      slots[k] = f;
+      f = (f + 1) % c->cfg.num_frames;
+    }
+    std::memcpy(c->header.data(), header, bytes);  // as the per-frame calls leave it
+    const int prog = mode == RT_MODE_PHONG ? RT_PROG_P_COMPUTE : RT_PROG_H_COMPUTE;
+    // at most F frames per launch: each colour slot is written by one frame of a launch (frames
+    // k and k + F of one launch would race for slot k % F)
+    const int mb = std::min(rt::kMaxBatch, c->cfg.num_frames);
+    for (int k0 = 0; k0 < n; k0 += mb) {
+      const int m = std::min(mb, n - k0);
+      int rc = run_program_mf(c, prog, slots[k0], m, lights.data() + k0);
+      if (rc != RT_OK) return rc;
+    }
+    return f;
   }
+  if (c->pipelined || n < 2) {  // pipelined mode 1 rotates its own header copies per frame
+    for (int k = 0; k < n; ++k) {
+      int rc = update(k, frame);
+      if (rc == RT_OK) rc = rt_upload_header(c, header, bytes);
+      if (rc != RT_OK) return rc;
+      frame = rt_dispatch(c, mode, frame);
+      if (frame < 0) return frame;
+    }
+    return frame;
+  }
+  // Sequential frames in batches: the host updates of up to kBatch frames are packed into
+  // consecutive device table copies with ONE upload, then the frames' programs are launched
+  // back to back, each reading its own copy.  Per frame the host then only enqueues kernels,
+  // which keeps small frames (config (a): a ~9 us kernel) GPU-bound.
+  constexpr int kBatch = 32;
+  const size_t tv = c->table.size();
+  RT_HIP(c, hipSetDevice(c->device));
+  int jr = join(c);
+  if (jr != RT_OK) return jr;
+  if (!c->d_batch) RT_HIP(c, hipMalloc(&c->d_batch, (size_t)kBatch * tv * sizeof(float4)));
+  c->batch_host.resize((size_t)kBatch * tv);
+  c->batch_hdr.resize((size_t)kBatch * (bytes / sizeof(float)));
+  const int Sc = table_stride(c);
+  const size_t hf = bytes / sizeof(float);
+  for (int k0 = 0; k0 < n; k0 += kBatch) {
+    const int m = std::min(kBatch, n - k0);
+    std::vector<int> nobj(m), npl(m), slot(m);
+    int f = frame;
+    for (int j = 0; j < m; ++j) {
+      int rc = update(k0 + j, f);
+      if (rc == RT_OK) rc = pack_header(c, header, c->batch_host.data() + (size_t)j * tv, nobj[j], npl[j]);
+      if (rc != RT_OK) return rc;
+      std::memcpy(c->batch_hdr.data() + (size_t)j * hf, header, bytes);  // camera / light of frame j
+      slot[j] = f;
+      f = (f + 1) % c->cfg.num_frames;
+    }
+    int rc = staged_copy(c, c->d_batch, c->batch_host.data(), (size_t)m * tv * sizeof(float4), c->stream);
+    if (rc != RT_OK) return rc;
+    for (int j = 0; j < m; ++j) {
+      c->d_shapes = c->d_batch + (size_t)j * tv;
+      c->d_rb = c->d_shapes + rt::rand_table(Sc);
+      c->nobj = nobj[j];
+      c->nplanes = npl[j];
+      c->have_header = true;
+      std::memcpy(c->header.data(), c->batch_hdr.data() + (size_t)j * hf, bytes);  // launch parameters
+      frame = rt_dispatch(c, mode, slot[j]);
+      if (frame < 0) return frame;
+    }
+  }
+  // leave the context as the per-frame calls would: the last header in its own device copy
+  std::memcpy(c->header.data(), header, bytes);
+  std::memcpy(c->table.data(), c->batch_host.data() + (size_t)((n - 1) % kBatch) * tv, tv * sizeof(float4));
+  int rc = staged_copy(c, c->d_shapes_buf[0], c->table.data(), tv * sizeof(float4), c->stream);
+  if (rc != RT_OK) return rc;
+  c->d_shapes = c->d_shapes_buf[0];
+  c->d_rb = c->d_rb_buf[0];
   return frame;
 }
 
