@@ -22,17 +22,28 @@ def main():
             for key in ("ao_batch_kernel", "ao_kernel", "post_kernel", "phong_kernel", "hybrid_kernel"):
                 if key + "<" in name or key + "(" in name:
                     d = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6
+                    # one entry per instantiation (template arguments included): the counted
+                    # frames run the counter-enabled instantiation, with its own registers
+                    inst = name.split("(rt::FrameParams")[0].replace("void rt::(anonymous namespace)::", "")
+                    inst = inst.replace("rt::(anonymous namespace)::", "")
                     launches.setdefault(key, []).append((int(row["Dispatch_Id"]), d, row["VGPR_Count"],
-                                                         row["SGPR_Count"], row["LDS_Block_Size"]))
+                                                         row["SGPR_Count"], row["LDS_Block_Size"], inst))
     if cmd:
         print(cmd)
     print(f"per-launch durations (ms), in dispatch order: {warm} warm-up, {steps} timed, 2 standalone, "
           f"2 counted (work counters on)")
+    print("rocprof's VGPR_Count is about half the compiler's VGPR count (tools/resource_usage.py: the production "
+          "AO kernel 72 -> 36, post_kernel 56 -> 28) and LDS_Block_Size counts static LDS only")
     for key, ls in launches.items():
         ls.sort()
         ds = [d for _, d, *_ in ls]
         timed = ds[warm:warm + steps]
-        print(f"{key}: vgpr={ls[0][2]} sgpr={ls[0][3]} lds={ls[0][4]}")
+        insts = {}
+        for _, _, v, sg, lds, inst in ls:
+            insts.setdefault(inst, (v, sg, lds, 0))
+            insts[inst] = insts[inst][:3] + (insts[inst][3] + 1,)
+        for inst, (v, sg, lds, n) in insts.items():
+            print(f"{key}: {inst}: {n} launches, vgpr={v} sgpr={sg} lds(static)={lds}")
         print(f"  all={[round(d, 3) for d in ds]}")
         if timed:
             print(f"  timed mean={sum(timed) / len(timed):.4f} ms")
