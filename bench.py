@@ -146,6 +146,23 @@ def cpu_baseline(cfg_name: str, target_s: float) -> dict:
                       f"{t / (len(rows) * FR) * H * 1e3:.0f}"}
 
 
+VALU_FMA_RATE = 116.7e12 / 128  # wave64 v_fma_f32 instructions/s a dense stream sustains (profiles/r01g_valu_rate.txt)
+
+
+def load_sq(cfg_name: str, src_sha1):
+    """SQ counters per dispatch (profiles/*_sq_<cfg>.json, tools/pmc_config.sh), preferring this build's."""
+    found = []
+    for p in sorted(ROOT.glob(f"profiles/*_sq_{cfg_name}.json"), reverse=True):
+        try:
+            found.append((json.loads(p.read_text()), p.name))
+        except Exception:
+            continue
+    for data, name in found:
+        if src_sha1 and data.get("src_sha1") == src_sha1:
+            return data, name
+    return found[0] if found else (None, None)
+
+
 def build_info() -> dict:
     """The library's source hash and commit (written by `make lib` next to librtrt.so)."""
     try:
@@ -490,6 +507,19 @@ def main():
             "traffic_src_sha1": traffic_data.get("src_sha1") if traffic_data else None,
             "traffic_on_this_build": bool(traffic_data and traffic_data.get("src_sha1") == binfo.get("src_sha1")),
         }
+        # the hardware's view beside the algorithmic one: VALU wave-instructions the kernel issues
+        # per launch (SQ_INSTS_VALU, committed counter run) over what the launch could issue at
+        # the spec rate (1 wave64 FP32 FMA per 2 clocks per SIMD, the peak above) and at the rate
+        # a dense v_fma_f32 stream sustains on this GPU
+        sq, sq_src = load_sq(args.config, binfo.get("src_sha1"))
+        if sq:
+            kern = next(iter(sq["kernels"].values()))
+            insts = kern.get("SQ_INSTS_VALU")
+            if insts:
+                spec = PEAK_FP32_TFLOPS * 1e12 / 128 * avg_ms * 1e-3
+                roof["valu_issue"] = {"insts_per_launch": insts, "frac_of_spec_issue": round(insts / spec, 4),
+                                      "frac_of_sustained_fma_issue": round(insts / (VALU_FMA_RATE * avg_ms * 1e-3), 4),
+                                      "source": sq_src, "on_this_build": sq.get("src_sha1") == binfo.get("src_sha1")}
         out = {
             "metric": "Mrays/s + ms/frame at 3840x2160, 16 AO samples, 64 spheres; 1/2/4/8 GPU",
             "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
@@ -497,6 +527,7 @@ def main():
             "ms_per_step_median": round(float(np.median(intervals)), 4) if intervals else None,
             "ms_per_step_median_of": ("per-frame completion intervals (events on the output stream)" if not host_loop
                                       else f"{len(intervals)} chunks of the C++ frame loop") if intervals else None,
+            "frame_intervals_ms": [round(v, 3) for v in intervals] if not host_loop else None,
             "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": desc, "width": W, "height": H, "spheres": S, "spp": spp, "mode": mode,

@@ -32,7 +32,18 @@ for d in sorted(glob.glob(os.path.join(out, f"{cfg}_g*"))):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
             if ksub in k:
-                res[k.split("(")[0][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                name = k.replace("void ", "").replace("rt::(anonymous namespace)::", "").split("(rt::FrameParams")[0]
+                res[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+import json
+try:  # the library build the counters were taken on (make lib writes BUILD_INFO)
+    info = json.load(open(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "real_time_ray_tracer_amd", "BUILD_INFO")))
+except Exception:
+    info = {}
+out_json = {"config": cfg, "kernels": {}, "src_sha1": info.get("src_sha1"), "commit": info.get("commit"),
+            "units": "per dispatch, mean over the dispatches of the bench run (warm-up, timed, standalone, counted)"}
 for k, cs in res.items():
-    print(cfg, k, {c: round(sum(v) / len(v)) for c, v in sorted(cs.items())}, "dispatches", max(len(v) for v in cs.values()))
+    avg = {c: round(sum(v) / len(v)) for c, v in sorted(cs.items())}
+    print(cfg, k, avg, "dispatches", max(len(v) for v in cs.values()))
+    out_json["kernels"][k] = avg
+json.dump(out_json, open(os.path.join(out, f"sq_{cfg}.json"), "w"), indent=1)
 EOF
