@@ -385,9 +385,10 @@ def main():
     host_s = 0.0  # host time inside step() (enqueue + back-pressure waits)
     frame_ev = []  # per-frame completion events (the frame's last stream): median frame interval
     if host_loop:
-        # chunks of the C++ loop, each bracketed by an event: the median chunk's ms per frame
-        nch = min(args.steps, 5)
-        sizes = [args.steps // nch + (1 if i < args.steps % nch else 0) for i in range(nch)]
+        # chunks of the C++ loop, each bracketed by an event: the median chunk's ms per frame;
+        # chunks of F frames (a multi-frame launch of modes 2-4 never spans two chunks)
+        F = rend.F
+        sizes = [min(F, args.steps - i) for i in range(0, args.steps, F)]
         k0 = warm
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(stream)

@@ -57,6 +57,9 @@ struct FrameParams {
   // the image.  The shape table is the same for every frame of the batch.
   int mf_n, mf_slot0;
   float4 mf_light[kMaxBatch];
+  // multi-frame AO launch (mode 2, gridDim.y = mf_n): frame j reads rand_buffer mf_rb[j * 2 spp ..]
+  // and writes slot (mf_slot0 + j) % F (hist_pix / hist_nrm / hist_dep); the image by frame mf_n - 1
+  const float4* mf_rb;
 };
 
 // Device shape table of one header copy, in float4 units from its base (rt_shim fills it):

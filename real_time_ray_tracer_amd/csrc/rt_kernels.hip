@@ -930,14 +930,26 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
 
 // geo: the sphere table (P.sph).  PL: the scene has planes, tested after the spheres of every
 // segment (plane_candidate) and, for the primary rays, culled against the pool cone.
+// MF: frame blockIdx.y of a multi-frame mode-2 launch (FrameParams::mf_rb): its own rand_buffer
+// and slot buffers, the image by the launch's last frame only.
 template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
-          int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false>
+          int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   // CNT = false: the work counters compiled out (timed launches pass none): fewer live scalars
   unsigned long long* const cnts = CNT ? P.counters : nullptr;
   unsigned long long* const rowc = CNT ? P.row_counters : nullptr;
   extern __shared__ float4 lds[];
   const int spp = SPPC ? SPPC : P.spp, W = P.W, D = P.D, nobj = P.nobj;
+  // this frame's buffers (the launch's frame unless MF)
+  const int fj = MF ? (int)blockIdx.y : 0;
+  const int fslot = MF ? (P.mf_slot0 + fj) % P.F : 0;
+  float4* const f_nrm = MF ? (float4*)P.hist_nrm[fslot] : P.nrm;
+  float4* const f_dep = MF ? (float4*)P.hist_dep[fslot] : P.dep;
+  const float4* const f_nrm_prev = MF ? f_nrm : P.nrm_prev;  // sequential frames: the slot itself
+  const float4* const f_dep_prev = MF ? f_dep : P.dep_prev;
+  float4* const f_out = MF ? (float4*)P.hist_pix[fslot] : P.out_pix;
+  float4* const f_img = MF ? (fj == P.mf_n - 1 ? P.image : nullptr) : P.image;
+  const float4* const f_rb = MF ? P.mf_rb + (size_t)fj * 2 * spp : P.rb;
   const int TP = POOL / spp > 0 ? POOL / spp : 1;
   const int lane = threadIdx.x;
   const int NS = TP * spp;
@@ -950,7 +962,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   int* perm = (int*)(lbase + LO.perm);
   unsigned long long* cmask = (unsigned long long*)(lbase + LO.cmask);
   float4* rls = (float4*)(lbase + LO.rls);
-  for (int k = lane; k < 2 * spp; k += 64) rls[k] = P.rb[k];
+  for (int k = lane; k < 2 * spp; k += 64) rls[k] = f_rb[k];
   for (int k = lane; k < TP; k += 64) pstop[k] = -1;
   // TAIL: the sphere table in LDS (per-lane sphere indices in the split tail rounds)
   float4* geol = (float4*)(lbase + LO.geol);  // [nobj] when TAIL && nobj <= kTailMaxObj
@@ -1031,9 +1043,9 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       int x, y;
       pool_xy(lp, x, y);
       const size_t off = (size_t)(y - P.band_row0) * W + x;
-      P.nrm[off] = z;
-      P.dep[off] = z;  // (0, 0, 0, 0) / AA
-      store_color(P, x, y, col);
+      f_nrm[off] = z;
+      f_dep[off] = z;  // (0, 0, 0, 0) / AA
+      store_color(P, f_out, f_img, x, y, col);
       if (rowc) atomicAdd(&rowc[y - P.band_row0], (unsigned long long)spp);  // ~free
     }
     if (cnts && lane == 0) {
@@ -1402,18 +1414,18 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     if (kind == PRIM_HIT) {
       float4 r0 = prec[lp];
       d = make_float4(r0.w, 0.0f, 0.0f, 1.0f);
-      P.nrm[off] = make_float4(r0.x, r0.y, r0.z, 1.0f);
+      f_nrm[off] = make_float4(r0.x, r0.y, r0.z, 1.0f);
     } else if (kind == PRIM_MISS) {
       d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      P.nrm[off] = d;
-    } else {  // stale (see ao_kernel)
-      d = P.dep_prev[off];
-      if (P.nrm_prev != P.nrm) P.nrm[off] = P.nrm_prev[off];
+      f_nrm[off] = d;
+    } else {  // stale: the slot's previous normal / depth (an emissive first hit writes neither)
+      d = f_dep_prev[off];
+      if (f_nrm_prev != f_nrm) f_nrm[off] = f_nrm_prev[off];
     }
     if (ystop >= 0.0f) d.y = ystop;
     d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
-    P.dep[off] = d;
-    store_color(P, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
+    f_dep[off] = d;
+    store_color(P, f_out, f_img, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
   }
   if (ABL == 3 && cnts && lane == 0) {
     lap(4);
@@ -1953,6 +1965,14 @@ size_t tab_lds_bytes(const FrameParams& p) { return (size_t)5 * (p.nobj > 0 ? p.
 // planes (PL).
 template <int SPPC, bool PL>
 void launch_batch(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStream_t stream, const FrameParams& q) {
+  if (q.mf_n > 0) {  // multi-frame mode-2 launch (never with counters: rt_compute_frames checks)
+    g.y = (unsigned)q.mf_n;
+    if (tl)
+      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL, true>), g, b, lds, stream, q, q.sph);
+    else
+      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, SPPC, false, false, PL, true>), g, b, lds, stream, q, q.sph);
+    return;
+  }
   if (tl && cnt)
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, true, PL>), g, b, lds, stream, q, q.sph);
   else if (tl)

@@ -91,6 +91,7 @@ struct rt_ctx {
   bool have_header = false;
   int nplanes = 0;             // planes among simple_shapes[0, nobj)
   float4* d_batch = nullptr;   // rt_compute_frames: a batch of device table copies (one per frame)
+  float4* d_mf_rb = nullptr;   // rt_compute_frames, mode 2: the rand_buffers of a multi-frame launch
   std::vector<float4> batch_host;
   std::vector<float> batch_hdr;  // the batch's host headers (camera, light: launch parameters)
   int nobj = 0;
@@ -197,6 +198,7 @@ void free_all(rt_ctx* c) {
   }
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->d_batch) (void)hipFree(c->d_batch);
+  if (c->d_mf_rb) (void)hipFree(c->d_mf_rb);
   if (c->d_row_counters) (void)hipFree(c->d_row_counters);
   for (auto e : {c->ev_ao, c->ev_join, c->ev_seq})
     if (e) (void)hipEventDestroy(e);
@@ -348,13 +350,14 @@ int run_program(rt_ctx* c, int program, int frame) {
   }
 }
 
-// Frames slot0, slot0+1, ... (m <= min(kMaxBatch, F), one light each) of a Phong/hybrid program
-// in ONE launch (gridDim.z = m).  The frames of modes 3/4 are independent (each writes its own colour
-// slot; the g-buffer normals/depth are not touched), so they may run concurrently; the image,
-// which the next frame would overwrite, is written by the last frame only.
+// Frames slot0, slot0+1, ... (m <= min(kMaxBatch, F)) of one program in ONE launch: Phong /
+// hybrid (gridDim.z = m, one light each) or ao_compute (gridDim.y = m, one rand_buffer each,
+// from d_mf_rb).  The frames of modes 2-4 touch only their own slot (mode 2's stale-depth reads
+// come from the slot's previous contents, F frames back), so they may run concurrently; the
+// image, which each next frame overwrites, is written by the last frame only.
 int run_program_mf(rt_ctx* c, int program, int slot0, int m, const float4* lights) {
   if (!c->have_header) return RT_E_STATE;
-  if (program != RT_PROG_P_COMPUTE && program != RT_PROG_H_COMPUTE) return RT_E_INVAL;
+  if (program != RT_PROG_P_COMPUTE && program != RT_PROG_H_COMPUTE && program != RT_PROG_AO_COMPUTE) return RT_E_INVAL;
   if (m < 1 || m > rt::kMaxBatch || m > c->cfg.num_frames || slot0 < 0 || slot0 >= c->cfg.num_frames)
     return RT_E_INVAL;
   RT_HIP(c, hipSetDevice(c->device));
@@ -362,12 +365,15 @@ int run_program_mf(rt_ctx* c, int program, int slot0, int m, const float4* light
   if (jr != RT_OK) return jr;
   rt::FrameParams p;
   fill_params(c, slot0, p);
-  p.trace_row0 = c->own0;
-  p.trace_rows = c->own_rows;
+  const bool ao = program == RT_PROG_AO_COMPUTE;
+  p.trace_row0 = ao ? c->band0 : c->own0;  // g-buffer writers trace the halo rows too (run_program)
+  p.trace_rows = ao ? c->band_rows : c->own_rows;
   p.out_pix = c->pix[c->pix_slot[slot0]];
   p.mf_n = m;
   p.mf_slot0 = slot0;
-  for (int j = 0; j < m; ++j) p.mf_light[j] = lights[j];
+  if (ao) p.mf_rb = c->d_mf_rb;
+  else
+    for (int j = 0; j < m; ++j) p.mf_light[j] = lights[j];
   return launch(c, program, p);
 }
 
@@ -802,6 +808,36 @@ int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint
       int rc = run_program_mf(c, prog, slots[k0], m, lights.data() + k0);
       if (rc != RT_OK) return rc;
     }
+    return f;
+  }
+  if (mode == RT_MODE_AO && n >= 2 && !c->counting && !c->row_counting) {
+    // Mode 2: the per-frame host update replaces only rand_buffer (fill_rand_buffer,
+    // src/main.cpp:535-539) and mode.y, so the shape table is uploaded once and up to F frames
+    // go in one launch, each with its own rand_buffer (run_program_mf).
+    const int nrb = 2 * spp;
+    std::vector<float4> rbs((size_t)n * nrb);
+    std::vector<int> slots(n);
+    int f = frame;
+    for (int k = 0; k < n; ++k) {
+      int rc = update(k, f);
+      if (rc == RT_OK && k == 0) rc = rt_upload_header(c, header, bytes);
+      if (rc != RT_OK) return rc;
+      std::memcpy(&rbs[(size_t)k * nrb], header + rt_off_rand(S) / 4, (size_t)nrb * sizeof(float4));
+      slots[k] = f;
+      f = (f + 1) % c->cfg.num_frames;
+    }
+    RT_HIP(c, hipSetDevice(c->device));
+    if (!c->d_mf_rb) RT_HIP(c, hipMalloc(&c->d_mf_rb, (size_t)rt::kMaxBatch * nrb * sizeof(float4)));
+    const int mb = std::min(rt::kMaxBatch, c->cfg.num_frames);
+    for (int k0 = 0; k0 < n; k0 += mb) {
+      const int m = std::min(mb, n - k0);
+      int rc = staged_copy(c, c->d_mf_rb, &rbs[(size_t)k0 * nrb], (size_t)m * nrb * sizeof(float4), c->stream);
+      if (rc == RT_OK) rc = run_program_mf(c, RT_PROG_AO_COMPUTE, slots[k0], m, nullptr);
+      if (rc != RT_OK) return rc;
+    }
+    // leave the context as the per-frame calls would: the last header uploaded
+    int rc = rt_upload_header(c, header, bytes);
+    if (rc != RT_OK) return rc;
     return f;
   }
   if (c->pipelined || n < 2) {  // pipelined mode 1 rotates its own header copies per frame
