@@ -979,15 +979,38 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   const float4* aux = P.shapes + 3 * P.S;
 
   const long long npix = (long long)P.trace_rows * W;
-  const long long p0 = (long long)blockIdx.x * TP;
+  // pool of this workgroup: blockIdx.x, or with pool_ilv = k > 1 the k-way interleave of the
+  // frame's pools (consecutive workgroups take pools from k evenly spaced bands; a bijection)
+  unsigned pb = blockIdx.x;
+  if (P.pool_ilv > 1) {
+    const unsigned k = (unsigned)P.pool_ilv, q = gridDim.x / k;
+    if (pb < q * k) pb = (pb % k) * q + pb / k;
+  }
+  // XCD balance: workgroups are dealt round-robin to the 8 XCDs (b mod 8), so in row order an XCD
+  // would take the same pool columns in every row (the same 16-px column stripes of the image);
+  // rotating row r's pools by r (groups of pool_rot = pools per row) moves each XCD's columns by
+  // one pool per row, so over 8 rows every XCD samples every column residue (a bijection on the
+  // full groups; the last, partial group keeps its order).  Config (d) AO launch: -3%.
+  if (P.pool_rot > 0) {
+    const unsigned Q = (unsigned)P.pool_rot, r = pb / Q;
+    if ((r + 1) * Q <= gridDim.x) {
+      unsigned c = pb - r * Q + r % Q;
+      c = c >= Q ? c - Q : c;
+      pb = r * Q + c;
+    }
+  }
+  const long long p0 = (long long)pb * TP;
   const int np = (int)(npix - p0 < TP ? npix - p0 : TP);
   const int total = np * spp;
 
   // ABL == 3: per-section wave clock (s_memtime) into the counters, timing ablation only
   unsigned long long tsec[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // 5..7: bounce rounds, sum ncull, prepares
-  unsigned long long tmark = ABL == 3 ? __builtin_amdgcn_s_memtime() : 0;
+  // ABL == 6: the same, with slots 5..7 timing the batched first bounce's cone + cull, survivor
+  // loop and shading; ABL == 7: event counts of the first bounce and the bounce rounds instead
+  constexpr bool kLaps = ABL == 3 || ABL == 6;
+  unsigned long long tmark = kLaps ? __builtin_amdgcn_s_memtime() : 0;
   auto lap = [&](int k) {
-    if (ABL == 3) {
+    if (kLaps) {
       unsigned long long now = __builtin_amdgcn_s_memtime();
       tsec[k] += now - tmark;
       tmark = now;
@@ -1048,7 +1071,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       store_color(P, f_out, f_img, x, y, col);
       if (rowc) atomicAdd(&rowc[y - P.band_row0], (unsigned long long)spp);  // ~free
     }
-    if (cnts && lane == 0) {
+    if (cnts && lane == 0 && ABL < 3) {  // (ABL >= 3: the counters hold section clocks / events)
       unsigned long long* c = cnts + (blockIdx.x & (kCounterSlots - 1));
       atomicAdd(&c[0 * kCounterSlots], (unsigned long long)total);
       atomicAdd(&c[1 * kCounterSlots], (unsigned long long)total);
@@ -1217,10 +1240,10 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           // this loop's per-lane addresses live across the whole pool and spills them to scratch
           const int i = (w << 6) + lane_id_here();
           bool keep;
+          float4 pt;
           if (pt_ok) {
-            float4 pt;
             keep = i < nobj && bounce_cone_keep_pt(cb, geo[i], pt);
-            if (i < nobj) geol[i] = pt;
+            if (ABL < 8 && i < nobj) geol[i] = pt;
           } else {
             keep = i < nobj && !bounce_cone_misses(cb, geo[i]);
           }
@@ -1231,18 +1254,60 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           exec_tests += (unsigned long long)__popcll(m);
           b1cost += __popcll(m);
           if (ABL == 3) tsec[6] += (unsigned long long)__popcll(m) << 24;  // sections: first-bounce survivors
-          if (pt_ok) {
+          if (pt_ok && ABL >= 8) {
+            // pass 1: the survivors some live lane's ray passes the pre-test for (row j read from
+            // lane j's registers: no LDS round trip per survivor); pass 2: the exact test of
+            // those only, by every live lane, ascending (a lane failing the pre-test cannot
+            // accept the sphere, nor can any lane a survivor whose pre-test no lane passes)
+            unsigned long long any = 0, mm = m;
+            while (mm) {
+              const int j = __builtin_ctzll(mm);
+              mm &= mm - 1;
+              const float ux = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pt.x), j));
+              const float uy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pt.y), j));
+              const float uz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pt.z), j));
+              const float kk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pt.w), j));
+              const bool pass = live && fmaf(bdir.z, uz, fmaf(bdir.y, uy, bdir.x * ux)) >= kk;
+              if (__ballot(pass) != 0) any |= 1ull << j;
+            }
+            if (ABL == 6) lap(5);
+            const int base = w << 6, nw = nobj - base < 64 ? nobj - base : 64;
+            if (live) {
+              if (ABL == 8) {
+                closest_hit_pf_masked(geo + base, nw, base, any, bpos, bdir, 0.0001f, t, ind);
+              } else {
+                while (any) {
+                  const int k = base + __builtin_ctzll(any);
+                  any &= any - 1;
+                  sphere_candidate(bpos, bdir, geo[k], k, 0.0001f, t, ind);
+                }
+              }
+            }
+          } else if (pt_ok) {
             geol_valid = false;
             __syncthreads();  // the pre-test rows are written
+            if (ABL == 6) lap(5);
             if (live)
               while (m) {
                 const int k = (w << 6) + __builtin_ctzll(m);
                 m &= m - 1;
                 const float4 q = geol[k];  // wave-uniform address: LDS broadcast
                 const float4 g = geo[k];
+                if (ABL == 7) {  // survivor iterations; with any pre-test pass; with any del >= 0 there
+                  const bool pass = fmaf(bdir.z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w;
+                  const f3 pmc = bpos - xyz(g);
+                  const float bb = dot(bdir, pmc);
+                  const float del = fmaf(g.w, g.w, fmaf(bb, bb, -dot(pmc, pmc)));
+                  const unsigned long long pm = __ballot(pass), dm = __ballot(pass && del >= 0.0f);
+                  tsec[0] += 1; tsec[1] += pm != 0; tsec[2] += dm != 0;
+                  tsec[3] += (unsigned long long)__popcll(pm);
+                }
+                if (ABL == 5)  // both loads in flight before the first wait (one latency, not two)
+                  asm volatile("" ::"v"(q.x), "v"(q.y), "v"(q.z), "v"(q.w), "s"(g.x), "s"(g.y), "s"(g.z), "s"(g.w));
                 if (fmaf(bdir.z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w)
                   sphere_candidate(bpos, bdir, g, k, 0.0001f, t, ind);
               }
+            if (ABL == 6) lap(6);
           } else if (live) {
             while (m) {
               const int k = (w << 6) + __builtin_ctzll(m);
@@ -1251,11 +1316,13 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
             }
           }
         }
+        if (ABL == 7) { tsec[4] += 1; tsec[5] += (unsigned long long)__popcll(lm1); }
         if (live) {
           if (PL) plane_pass(P, bpos, bdir, 0.0001f, t, ind);
           ++nseg;
           live = shade(ind, t, bpos, bdir, bhemi, br, bg, bb, D - 1, bitem, false);
         }
+        if (ABL == 6) lap(7);
         bdepth = D - 2;
         lap(4);  // sections: the batched first bounce (shares slot 4 with combine + stores)
       }
@@ -1352,9 +1419,19 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     }
     // ---- one bounce segment for every live path, against every sphere ------------------
     exec_tests += (unsigned long long)nobj;
+    if (ABL == 7) {  // later bounce rounds: sphere iterations, and those with any live lane's del >= 0
+      tsec[6] += (unsigned long long)nobj;
+      for (int i = 0; i < nobj; ++i) {
+        const float4 g = geo[i];
+        const f3 pmc = pos - xyz(g);
+        const float bb = dot(dir, pmc);
+        const float del = fmaf(g.w, g.w, fmaf(bb, bb, -dot(pmc, pmc)));
+        tsec[7] += __ballot(has && del >= 0.0f) != 0;
+      }
+    }
     if (has) {
       float t;
-      int ind = closest_hit_pf2(geo, nobj, pos, dir, 0.0001f, t);
+      int ind = closest_hit_pf2<ABL == 4>(geo, nobj, pos, dir, 0.0001f, t);
       if (PL) plane_pass(P, pos, dir, 0.0001f, t, ind);
       if (ABL == 1) {  // timing ablation: the bounce tests twice
         float z, t2;
@@ -1370,7 +1447,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   }
   lap(2);
 
-  if (cnts && ABL != 3) {
+  if (cnts && !kLaps && ABL != 7) {
     unsigned sg = wave_sum(nseg);
     if (lane == 0) {
       unsigned long long* c = cnts + (blockIdx.x & (kCounterSlots - 1));
@@ -1427,7 +1504,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     f_dep[off] = d;
     store_color(P, f_out, f_img, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
   }
-  if (ABL == 3 && cnts && lane == 0) {
+  if ((kLaps || ABL == 7) && cnts && lane == 0) {
     lap(4);
     unsigned long long* c = cnts + (blockIdx.x & (kCounterSlots - 1));
     for (int k = 0; k < 8; ++k) atomicAdd(&c[k * kCounterSlots], tsec[k]);
@@ -1996,6 +2073,10 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
   const int variant = ev ? atoi(ev) : 7;
   const char* eb = getenv("RTRT_B1_MIN");
   q.b1_min = eb ? atoi(eb) : 1;
+  const char* ei = getenv("RTRT_POOL_ILV");
+  q.pool_ilv = ei ? atoi(ei) : 0;
+  const char* er = getenv("RTRT_POOL_ROT");
+  if (er && atoi(er) == 0) q.pool_rot = 0;  // A/B: pools in plain row order
   const char* eg = getenv("RTRT_GENERAL");
   const bool general = (eg && atoi(eg) == 1) || variant == 0 || variant == 2;
   const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
@@ -2022,7 +2103,7 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
       hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, false, true, 0, false, true, true>), g, b, pl_sh, stream, q, q.sph);
     return true;
   }
-  const size_t psh = (size_t)batch_lds(p.spp, kPool, (variant == 9 || variant == 27 || variant == 93) && tl ? p.nobj : 0).total;
+  const size_t psh = (size_t)batch_lds(p.spp, kPool, (variant == 9 || variant == 27 || variant >= 93) && tl ? p.nobj : 0).total;
   if (variant == 9 && p.spp == 16 && tl)  // 7 without the per-ray first-bounce pre-test
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 16, false, false>), g, b, psh, stream, q, q.sph);
   else if (variant == 27 && tl)  // 7 without the batched first bounce
@@ -2033,6 +2114,18 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 1>), g, b, psh, stream, q, q.sph);
   else if (variant == 92)
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2>), g, b, psh, stream, q, q.sph);
+  else if (variant == 96 && tl && p.spp == 16)  // section clocks, first bounce split in 3
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 6, true, true, 16, true>), g, b, psh, stream, q, q.sph);
+  else if (variant == 97 && tl && p.spp == 16)  // first-bounce / bounce-round event counts
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 7, true, true, 16, true>), g, b, psh, stream, q, q.sph);
+  else if (variant == 98 && tl && p.spp == 16)  // first bounce: pre-test rows by readlane, masked exact pass
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 8, true, true, 16, true, false>), g, b, psh, stream, q, q.sph);
+  else if (variant == 99 && tl && p.spp == 16)  // the same, pass 2 as a plain loop over the set bits
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 9, true, true, 16, true, false>), g, b, psh, stream, q, q.sph);
+  else if (variant == 95 && tl && p.spp == 16)  // first-bounce survivor loads waited together
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 5, true, true, 16, true, false>), g, b, psh, stream, q, q.sph);
+  else if (variant == 94 && tl && p.spp == 16)  // branchless hit tails in the later bounce rounds
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 4, true, true, 16, true, false>), g, b, psh, stream, q, q.sph);
   else if (variant == 93 && tl && p.spp == 16)  // section clocks of the production kernel
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true, 16, true>), g, b, psh, stream, q, q.sph);
   else if (variant == 93 && tl)
@@ -2066,6 +2159,12 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
   q.sph = p.shapes + sphere_table(p.S);
   q.planes = p.shapes + plane_table(p.S);
   q.b1_min = 1;
+  q.pool_ilv = 0;
+  {  // rotation group: the pools of one image row (at least 8)
+    const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
+    const int ppr = p.W / TP;
+    q.pool_rot = ppr >= 8 ? ppr : 8;
+  }
   const bool pl = p.nplanes > 0;
   if (program == K_AOP || program == K_AO) {
     const long long npix = (long long)p.trace_rows * p.W;

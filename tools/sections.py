@@ -3,6 +3,8 @@
 (RTRT_AO_VARIANT=93, s_memtime laps per section summed over waves) on a bench config.
 
     python tools/sections.py --config d --frames 3
+    python tools/sections.py --config d --variant 96   # the first bounce split into cull / survivors / shade
+    python tools/sections.py --config d --variant 97   # event counts: first-bounce survivors, bounce-round tails
 """
 import argparse
 import os
@@ -23,9 +25,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="d")
     ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--variant", default="93")
     a = ap.parse_args()
     W, H, S, spp, mode, _ = CONFIGS[a.config]
-    os.environ["RTRT_AO_VARIANT"] = "93"
+    os.environ["RTRT_AO_VARIANT"] = a.variant
     h = config_header(a.config)
     r = Renderer(W, H, S, spp)
     f = 0
@@ -38,6 +41,24 @@ def main():
         r.upload_header(h)
         f = r.dispatch(2 if mode == 1 else mode, f)  # AO pass only: counters 5..7 are the kernel's
     c = r.read_counters()
+    keys = ["samples", "segments", "shadow_rays", "tests", "executed_lane_tests", "post_pixels", "history_read",
+            "history_accepted"]
+    if a.variant == "97":
+        v = [c[k] for k in keys]
+        print(f"first bounce: {v[4]} batches, {v[5] / max(v[4], 1):.1f} live lanes per batch, "
+              f"{v[0] / max(v[4], 1):.2f} survivor iterations per batch")
+        print(f"  survivor iterations with any pre-test pass {v[1] / max(v[0], 1):.3f}, with any del >= 0 among "
+              f"the passing lanes {v[2] / max(v[0], 1):.3f}; lanes passing per iteration {v[3] / max(v[0], 1):.2f}")
+        print(f"bounce rounds: {v[6]} sphere iterations, any live lane del >= 0 in {v[7] / max(v[6], 1):.3f}")
+        return
+    if a.variant == "96":
+        names = ["cull setup", "prepare (primary + first shade)", "hand-out / regeneration", "bounce test + shade",
+                 "combine + stores", "first bounce: cone + cull", "first bounce: survivor tests",
+                 "first bounce: shade"]
+        v = [c[k] for k in keys]
+        for n, x in zip(names, v):
+            print(f"{n:34s} {x / 1e9:9.3f} Gclk  {100 * x / sum(v):5.1f}%")
+        return
     vals = [c["samples"], c["segments"], c["shadow_rays"], c["tests"], c["executed_lane_tests"]]
     tot = sum(vals)
     for n, v in zip(NAMES, vals):

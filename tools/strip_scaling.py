@@ -20,13 +20,24 @@ from real_time_ray_tracer_amd import Header, Renderer, aspect_for  # noqa: E402
 from real_time_ray_tracer_amd.dist import balanced_bounds, equal_bounds  # noqa: E402
 
 
-def frame_ms(W, H, S, spp, mode, h, rows, frames, warm=8, kernels=False):
+def frame_ms(W, H, S, spp, mode, h, rows, frames, warm=8, kernels=False, multi=False):
     r = Renderer(W, H, S, spp, rows=rows)
     if mode == 1 and not kernels:
         r.enable_pipelining(True)
     if kernels:
         r.enable_timing(True)
     f = 0
+    if multi:  # the render loop in C++ (rt_compute_frames): multi-frame launches for modes 2-4
+        f = r.compute_frames(h, mode, f, warm, 7000, False)
+        r.synchronize()
+        t0 = time.perf_counter()
+        f = r.compute_frames(h, mode, f, frames, 7000 + warm, False)
+        t_enq = time.perf_counter() - t0
+        r.synchronize()
+        ms = (time.perf_counter() - t0) / frames * 1e3
+        r.close()
+        frame_ms.host_ms = t_enq / frames * 1e3
+        return ms
     for k in range(warm + frames):
         if k == warm:
             r.synchronize()
@@ -55,14 +66,17 @@ def main():
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--equal", action="store_true")
     ap.add_argument("--kernels", action="store_true", help="sum of kernel times (sequential) instead of frame wall time")
+    ap.add_argument("--mode", type=int, default=0, help="override the config's mode (e.g. 2: the AO pass alone)")
+    ap.add_argument("--multi", action="store_true", help="frames through rt_compute_frames (multi-frame launches)")
     ap.add_argument("--only", type=int, default=-1, help="time only this strip (e.g. under rocprofv3)")
     ap.add_argument("--calibrate", action="store_true",
                     help="bench.py's calibration: time the plan's strips (pipelined frames for mode 1), rescale the profile, "
                          "re-balance; best of three measured plans")
     a = ap.parse_args()
     W, H, S, spp, mode, _ = CONFIGS[a.config]
+    mode = a.mode or mode
     h = config_header(a.config)
-    full = frame_ms(W, H, S, spp, mode, h, None, a.frames, kernels=a.kernels) if a.only < 0 else float("nan")
+    full = frame_ms(W, H, S, spp, mode, h, None, a.frames, kernels=a.kernels, multi=a.multi) if a.only < 0 else float("nan")
     if a.equal:
         b = equal_bounds(H, a.n)
     else:  # cost profile from the row counters of one whole-frame probe
@@ -90,7 +104,7 @@ def main():
     for i in range(a.n):
         if a.only >= 0 and i != a.only:
             continue
-        strips.append(frame_ms(W, H, S, spp, mode, h, (b[i], b[i + 1]), a.frames, kernels=a.kernels))
+        strips.append(frame_ms(W, H, S, spp, mode, h, (b[i], b[i + 1]), a.frames, kernels=a.kernels, multi=a.multi))
         host.append(frame_ms.host_ms)
     print(f"whole frame {full:.3f} ms; {a.n} strips {b}")
     print("strip ms", [round(t, 3) for t in strips])
