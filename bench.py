@@ -200,6 +200,10 @@ def main():
                          "overlapping frame k's post-process with frame k+1's AO pass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--warm-ms", type=float, default=300.0,
+                    help="after the warm-up frames, keep rendering (chunks of 8 frames) until this much wall "
+                         "time has passed on every rank, so the timed frames run at settled GPU clocks: the "
+                         "clock ramps over ~10 ms of load (DVFS), longer than 20 strip frames at N = 8")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 also renders every frame whole and checks the gathered frames bit for bit")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -254,6 +258,16 @@ def main():
                 frames = 24
             f = 0
             t0 = 0.0
+            if not counters:  # settled clocks for the measurement (see --warm-ms)
+                tw, k = time.perf_counter(), 0
+                while (time.perf_counter() - tw) * 1e3 < min(args.warm_ms, 100.0):
+                    header.fill_rand_buffer(7000 + k) if mode in (1, 2) else header.moving_light(False)
+                    header.set_mode(f, nobj)
+                    r.upload_header(header)
+                    f = r.dispatch(mode, f)
+                    k += 1
+                    if k % 8 == 0:
+                        r.synchronize()
             for k in range(frames):
                 header.fill_rand_buffer(7000 + k) if mode in (1, 2) else header.moving_light(False)
                 header.set_mode(f, nobj)
@@ -364,11 +378,29 @@ def main():
     # warm-up frames so the mode-1 temporal filter reads a full ring)
     ring_fill = max(0, rend.F - args.warmup)
     warm = args.warmup + ring_fill
+    tw = time.perf_counter()
     if host_loop:
         state["frame"] = rend.compute_frames(header, mode, state["frame"], warm, 7000, False)
     else:
         for k in range(warm):
             step(k)
+    # settle the clock: chunks of 8 more frames until warm_ms has passed on every rank (the
+    # ranks agree on the chunk count, so the per-frame gathers stay matched)
+    settle = 0
+    while True:
+        torch.cuda.synchronize()
+        left = torch.tensor([args.warm_ms - (time.perf_counter() - tw) * 1e3], dtype=torch.float64, device=cdev)
+        if world > 1:
+            dist.all_reduce(left, op=dist.ReduceOp.MAX)
+        if float(left.item()) <= 0.0:
+            break
+        if host_loop:
+            state["frame"] = rend.compute_frames(header, mode, state["frame"], 8, 7000 + warm + settle, False)
+        else:
+            for k in range(warm + settle, warm + settle + 8):
+                step(k)
+        settle += 8
+    warm += settle
     if gather is not None:
         gather.finish()
     torch.cuda.synchronize()
@@ -524,7 +556,8 @@ def main():
         out = {
             "metric": "Mrays/s + ms/frame at 3840x2160, 16 AO samples, 64 spheres; 1/2/4/8 GPU",
             "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ring_fill_frames": ring_fill, "ms_per_step": round(ms, 4),
+            "warmup": args.warmup, "ring_fill_frames": ring_fill, "settle_frames": settle,
+            "settle_ms": args.warm_ms, "ms_per_step": round(ms, 4),
             "ms_per_step_median": round(float(np.median(intervals)), 4) if intervals else None,
             "ms_per_step_median_of": ("per-frame completion intervals (events on the output stream)" if not host_loop
                                       else f"{len(intervals)} chunks of the C++ frame loop") if intervals else None,

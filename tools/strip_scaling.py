@@ -27,6 +27,17 @@ def frame_ms(W, H, S, spp, mode, h, rows, frames, warm=8, kernels=False, multi=F
     if kernels:
         r.enable_timing(True)
     f = 0
+    if frame_ms.warm_ms > 0:  # steady-state clocks: render for warm_ms of wall time first (DVFS ramp)
+        tw = time.perf_counter()
+        k = 0
+        while (time.perf_counter() - tw) * 1e3 < frame_ms.warm_ms:
+            h.fill_rand_buffer(7000 + k)
+            h.set_mode(f, h.num_objects)
+            r.upload_header(h)
+            f = r.dispatch(mode, f)
+            k += 1
+            if k % 8 == 0:
+                r.synchronize()
     if multi:  # the render loop in C++ (rt_compute_frames): multi-frame launches for modes 2-4
         f = r.compute_frames(h, mode, f, warm, 7000, False)
         r.synchronize()
@@ -59,6 +70,9 @@ def frame_ms(W, H, S, spp, mode, h, rows, frames, warm=8, kernels=False, multi=F
     return ms
 
 
+frame_ms.warm_ms = 0.0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="d")
@@ -67,6 +81,8 @@ def main():
     ap.add_argument("--equal", action="store_true")
     ap.add_argument("--kernels", action="store_true", help="sum of kernel times (sequential) instead of frame wall time")
     ap.add_argument("--mode", type=int, default=0, help="override the config's mode (e.g. 2: the AO pass alone)")
+    ap.add_argument("--warm-ms", type=float, default=0.0,
+                    help="render this long before timing each case, so the GPU clock has settled (DVFS ramp)")
     ap.add_argument("--multi", action="store_true", help="frames through rt_compute_frames (multi-frame launches)")
     ap.add_argument("--only", type=int, default=-1, help="time only this strip (e.g. under rocprofv3)")
     ap.add_argument("--calibrate", action="store_true",
@@ -75,6 +91,7 @@ def main():
     a = ap.parse_args()
     W, H, S, spp, mode, _ = CONFIGS[a.config]
     mode = a.mode or mode
+    frame_ms.warm_ms = a.warm_ms
     h = config_header(a.config)
     full = frame_ms(W, H, S, spp, mode, h, None, a.frames, kernels=a.kernels, multi=a.multi) if a.only < 0 else float("nan")
     if a.equal:
