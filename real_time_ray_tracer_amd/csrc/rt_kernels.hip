@@ -937,7 +937,24 @@ template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL =
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   // CNT = false: the work counters compiled out (timed launches pass none): fewer live scalars
   unsigned long long* const cnts = CNT ? P.counters : nullptr;
-  unsigned long long* const rowc = CNT ? P.row_counters : nullptr;
+  unsigned long long* const rowc = CNT && ABL != 10 ? P.row_counters : nullptr;
+  // ABL == 10 (A/B builds, tools/explore/xcd_balance.py): per-XCD wave start / end times in the
+  // row-counter buffer instead of the row costs
+  unsigned long long* const xr = ABL == 10 ? P.row_counters : nullptr;
+  const unsigned long long t_start = ABL == 10 ? __builtin_amdgcn_s_memrealtime() : 0;
+  auto xcd_mark = [&]() {
+    if (ABL == 10 && xr && threadIdx.x == 0) {
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      xcc &= 7u;
+      const unsigned long long te = __builtin_amdgcn_s_memrealtime();
+      atomicMax(&xr[2 * xcc], te);
+      atomicMax(&xr[2 * xcc + 1], ~t_start);
+      atomicAdd(&xr[16 + xcc], 1ull);
+      atomicAdd(&xr[24 + xcc], te - t_start);
+      if (blockIdx.x < 1024) xr[32 + blockIdx.x] = xcc + 1;  // the block -> XCD map of the first blocks
+    }
+  };
   extern __shared__ float4 lds[];
   const int spp = SPPC ? SPPC : P.spp, W = P.W, D = P.D, nobj = P.nobj;
   // this frame's buffers (the launch's frame unless MF)
@@ -991,6 +1008,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   // rotating row r's pools by r (groups of pool_rot = pools per row) moves each XCD's columns by
   // one pool per row, so over 8 rows every XCD samples every column residue (a bijection on the
   // full groups; the last, partial group keeps its order).  Config (d) AO launch: -3%.
+  if (ABL == 10 && P.pool_ilv < 0) pb = (unsigned)(-P.pool_ilv);  // XCD probe: every workgroup on one pool
   if (P.pool_rot > 0) {
     const unsigned Q = (unsigned)P.pool_rot, r = pb / Q;
     if ((r + 1) * Q <= gridDim.x) {
@@ -1077,6 +1095,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       atomicAdd(&c[1 * kCounterSlots], (unsigned long long)total);
       atomicAdd(&c[3 * kCounterSlots], (unsigned long long)total * (unsigned long long)nobj);
     }
+    xcd_mark();
     return;
   }
 
@@ -1504,6 +1523,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     f_dep[off] = d;
     store_color(P, f_out, f_img, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
   }
+  xcd_mark();
   if ((kLaps || ABL == 7) && cnts && lane == 0) {
     lap(4);
     unsigned long long* c = cnts + (blockIdx.x & (kCounterSlots - 1));
@@ -2118,6 +2138,8 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 6, true, true, 16, true>), g, b, psh, stream, q, q.sph);
   else if (variant == 97 && tl && p.spp == 16)  // first-bounce / bounce-round event counts
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 7, true, true, 16, true>), g, b, psh, stream, q, q.sph);
+  else if (variant == 100 && tl && p.spp == 16)  // per-XCD wave start / end times (row counters)
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 10, true, true, 16, true, true>), g, b, psh, stream, q, q.sph);
   else if (variant == 98 && tl && p.spp == 16)  // first bounce: pre-test rows by readlane, masked exact pass
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 8, true, true, 16, true, false>), g, b, psh, stream, q, q.sph);
   else if (variant == 99 && tl && p.spp == 16)  // the same, pass 2 as a plain loop over the set bits
@@ -2174,7 +2196,10 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
     const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
     const long long pools = (npix + TP - 1) / TP;
     const bool tl = p.nobj <= kTailMaxObj;
-    const size_t psh = (size_t)batch_lds(p.spp, kPool, tl ? p.nobj : 0).total;
+    size_t psh = (size_t)batch_lds(p.spp, kPool, tl ? p.nobj : 0).total;
+#if RTRT_AB
+    if (const char* el = getenv("RTRT_LDS_EXTRA")) psh += (size_t)atoi(el);  // LDS allocation-granule probe
+#endif
     const dim3 g((unsigned)pools), b(64);
     // timed launches pass no counters: the counter code is compiled out (fewer live scalars)
     const bool cnt = p.counters || p.row_counters;
