@@ -271,23 +271,6 @@ __device__ __forceinline__ void sphere_candidate(f3 pos, f3 dir, float4 g, int i
   }
 }
 
-// sphere_candidate without the branch: the hit tail runs on every lane, and a lane whose
-// discriminant is negative (or NaN) is excluded from the acceptance instead (thr >= 1e-6: the
-// tail's square root sees max(del, 2^-100), so a negative del yields some finite root that the
-// del >= 0 term rejects).  Same accepted t and index as sphere_candidate.
-__device__ __forceinline__ void sphere_candidate_nb(f3 pos, f3 dir, float4 g, int i, float thr, float& t, int& ind) {
-  f3 pmc = pos - xyz(g);
-  float b = dot(dir, pmc);
-  float del = fmaf(g.w, g.w, fmaf(b, b, -dot(pmc, pmc)));
-  float s = sqrt_rn_tail(del);
-  float t1 = -1.0f * b + s;
-  float t2 = -1.0f * b - s;
-  float res = __uint_as_float(min(__float_as_uint(t1), __float_as_uint(t2)));
-  const bool acc = (del >= 0.0f) & (res > thr) & (__float_as_uint(res) < __float_as_uint(t));
-  t = acc ? res : t;
-  ind = acc ? i : ind;
-}
-
 // One plane of the min-t scan, tested out of index order (after the spheres): plane_eval_ray
 // (p_compute.glsl:111-119) and the scan's acceptance, with the tie rule made explicit.  The
 // sequential scan (`res > thr && (res < t || t < 0)`, ascending i) ends with the accepted
@@ -387,13 +370,8 @@ __device__ __forceinline__ void closest_hit_pf_masked(const float4* __restrict__
 
 // closest_hit_pf with groups of 2 spheres (one s_load_dwordx8 each): half the scalar registers
 // of the 4-sphere pipeline.  Same visiting order and acceptance (bit-identical).
-template <bool NB = false>
 __device__ __forceinline__ int closest_hit_pf2(const float4* __restrict__ geo, int nobj, f3 pos, f3 dir, float thr,
                                                float& t_out) {
-  auto sphere_candidate = [](f3 pos, f3 dir, float4 g, int i, float thr, float& t, int& ind) {
-    if (NB) sphere_candidate_nb(pos, dir, g, i, thr, t, ind);
-    else ::rt::sphere_candidate(pos, dir, g, i, thr, t, ind);
-  };
   float t = -1.0f;
   int ind = -1;
   int i = 0;

@@ -20,7 +20,6 @@ struct FrameParams {
   int S;                     // stride of the compact shape table (capacity)
   int spp, D, F, frame;
   int b1_min;                // AO: least live lanes of a prepared batch for its batched first bounce (set at launch)
-  int pool_ilv;              // AO: pool interleave (0 = pools in row order; set at launch)
   int pool_rot;              // AO: pools per rotation group (one row's; 0 = pools in row order; set at launch)
   float inv_spp, fW, fH;     // 1.0f / spp, (float)W, (float)H: host-computed wave-uniform constants
   float inv_W, inv_H;        // 1.0f / fW, 1.0f / fH (correctly rounded; div_rn_by)

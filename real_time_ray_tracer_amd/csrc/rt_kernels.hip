@@ -937,24 +937,7 @@ template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL =
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   // CNT = false: the work counters compiled out (timed launches pass none): fewer live scalars
   unsigned long long* const cnts = CNT ? P.counters : nullptr;
-  unsigned long long* const rowc = CNT && ABL != 10 ? P.row_counters : nullptr;
-  // ABL == 10 (A/B builds, tools/explore/xcd_balance.py): per-XCD wave start / end times in the
-  // row-counter buffer instead of the row costs
-  unsigned long long* const xr = ABL == 10 ? P.row_counters : nullptr;
-  const unsigned long long t_start = ABL == 10 ? __builtin_amdgcn_s_memrealtime() : 0;
-  auto xcd_mark = [&]() {
-    if (ABL == 10 && xr && threadIdx.x == 0) {
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      xcc &= 7u;
-      const unsigned long long te = __builtin_amdgcn_s_memrealtime();
-      atomicMax(&xr[2 * xcc], te);
-      atomicMax(&xr[2 * xcc + 1], ~t_start);
-      atomicAdd(&xr[16 + xcc], 1ull);
-      atomicAdd(&xr[24 + xcc], te - t_start);
-      if (blockIdx.x < 1024) xr[32 + blockIdx.x] = xcc + 1;  // the block -> XCD map of the first blocks
-    }
-  };
+  unsigned long long* const rowc = CNT ? P.row_counters : nullptr;
   extern __shared__ float4 lds[];
   const int spp = SPPC ? SPPC : P.spp, W = P.W, D = P.D, nobj = P.nobj;
   // this frame's buffers (the launch's frame unless MF)
@@ -996,19 +979,13 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   const float4* aux = P.shapes + 3 * P.S;
 
   const long long npix = (long long)P.trace_rows * W;
-  // pool of this workgroup: blockIdx.x, or with pool_ilv = k > 1 the k-way interleave of the
-  // frame's pools (consecutive workgroups take pools from k evenly spaced bands; a bijection)
+  // pool of this workgroup
   unsigned pb = blockIdx.x;
-  if (P.pool_ilv > 1) {
-    const unsigned k = (unsigned)P.pool_ilv, q = gridDim.x / k;
-    if (pb < q * k) pb = (pb % k) * q + pb / k;
-  }
   // XCD balance: workgroups are dealt round-robin to the 8 XCDs (b mod 8), so in row order an XCD
   // would take the same pool columns in every row (the same 16-px column stripes of the image);
   // rotating row r's pools by r (groups of pool_rot = pools per row) moves each XCD's columns by
   // one pool per row, so over 8 rows every XCD samples every column residue (a bijection on the
   // full groups; the last, partial group keeps its order).  Config (d) AO launch: -3%.
-  if (ABL == 10 && P.pool_ilv < 0) pb = (unsigned)(-P.pool_ilv);  // XCD probe: every workgroup on one pool
   if (P.pool_rot > 0) {
     const unsigned Q = (unsigned)P.pool_rot, r = pb / Q;
     if ((r + 1) * Q <= gridDim.x) {
@@ -1095,7 +1072,6 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       atomicAdd(&c[1 * kCounterSlots], (unsigned long long)total);
       atomicAdd(&c[3 * kCounterSlots], (unsigned long long)total * (unsigned long long)nobj);
     }
-    xcd_mark();
     return;
   }
 
@@ -1259,10 +1235,10 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           // this loop's per-lane addresses live across the whole pool and spills them to scratch
           const int i = (w << 6) + lane_id_here();
           bool keep;
-          float4 pt;
           if (pt_ok) {
+            float4 pt;
             keep = i < nobj && bounce_cone_keep_pt(cb, geo[i], pt);
-            if (ABL < 8 && i < nobj) geol[i] = pt;
+            if (i < nobj) geol[i] = pt;
           } else {
             keep = i < nobj && !bounce_cone_misses(cb, geo[i]);
           }
@@ -1273,36 +1249,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           exec_tests += (unsigned long long)__popcll(m);
           b1cost += __popcll(m);
           if (ABL == 3) tsec[6] += (unsigned long long)__popcll(m) << 24;  // sections: first-bounce survivors
-          if (pt_ok && ABL >= 8) {
-            // pass 1: the survivors some live lane's ray passes the pre-test for (row j read from
-            // lane j's registers: no LDS round trip per survivor); pass 2: the exact test of
-            // those only, by every live lane, ascending (a lane failing the pre-test cannot
-            // accept the sphere, nor can any lane a survivor whose pre-test no lane passes)
-            unsigned long long any = 0, mm = m;
-            while (mm) {
-              const int j = __builtin_ctzll(mm);
-              mm &= mm - 1;
-              const float ux = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pt.x), j));
-              const float uy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pt.y), j));
-              const float uz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pt.z), j));
-              const float kk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pt.w), j));
-              const bool pass = live && fmaf(bdir.z, uz, fmaf(bdir.y, uy, bdir.x * ux)) >= kk;
-              if (__ballot(pass) != 0) any |= 1ull << j;
-            }
-            if (ABL == 6) lap(5);
-            const int base = w << 6, nw = nobj - base < 64 ? nobj - base : 64;
-            if (live) {
-              if (ABL == 8) {
-                closest_hit_pf_masked(geo + base, nw, base, any, bpos, bdir, 0.0001f, t, ind);
-              } else {
-                while (any) {
-                  const int k = base + __builtin_ctzll(any);
-                  any &= any - 1;
-                  sphere_candidate(bpos, bdir, geo[k], k, 0.0001f, t, ind);
-                }
-              }
-            }
-          } else if (pt_ok) {
+          if (pt_ok) {
             geol_valid = false;
             __syncthreads();  // the pre-test rows are written
             if (ABL == 6) lap(5);
@@ -1321,8 +1268,6 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
                   tsec[0] += 1; tsec[1] += pm != 0; tsec[2] += dm != 0;
                   tsec[3] += (unsigned long long)__popcll(pm);
                 }
-                if (ABL == 5)  // both loads in flight before the first wait (one latency, not two)
-                  asm volatile("" ::"v"(q.x), "v"(q.y), "v"(q.z), "v"(q.w), "s"(g.x), "s"(g.y), "s"(g.z), "s"(g.w));
                 if (fmaf(bdir.z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w)
                   sphere_candidate(bpos, bdir, g, k, 0.0001f, t, ind);
               }
@@ -1450,7 +1395,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     }
     if (has) {
       float t;
-      int ind = closest_hit_pf2<ABL == 4>(geo, nobj, pos, dir, 0.0001f, t);
+      int ind = closest_hit_pf2(geo, nobj, pos, dir, 0.0001f, t);
       if (PL) plane_pass(P, pos, dir, 0.0001f, t, ind);
       if (ABL == 1) {  // timing ablation: the bounce tests twice
         float z, t2;
@@ -1523,7 +1468,6 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     f_dep[off] = d;
     store_color(P, f_out, f_img, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
   }
-  xcd_mark();
   if ((kLaps || ABL == 7) && cnts && lane == 0) {
     lap(4);
     unsigned long long* c = cnts + (blockIdx.x & (kCounterSlots - 1));
@@ -2093,8 +2037,6 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
   const int variant = ev ? atoi(ev) : 7;
   const char* eb = getenv("RTRT_B1_MIN");
   q.b1_min = eb ? atoi(eb) : 1;
-  const char* ei = getenv("RTRT_POOL_ILV");
-  q.pool_ilv = ei ? atoi(ei) : 0;
   const char* er = getenv("RTRT_POOL_ROT");
   if (er && atoi(er) == 0) q.pool_rot = 0;  // A/B: pools in plain row order
   const char* eg = getenv("RTRT_GENERAL");
@@ -2138,16 +2080,6 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 6, true, true, 16, true>), g, b, psh, stream, q, q.sph);
   else if (variant == 97 && tl && p.spp == 16)  // first-bounce / bounce-round event counts
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 7, true, true, 16, true>), g, b, psh, stream, q, q.sph);
-  else if (variant == 100 && tl && p.spp == 16)  // per-XCD wave start / end times (row counters)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 10, true, true, 16, true, true>), g, b, psh, stream, q, q.sph);
-  else if (variant == 98 && tl && p.spp == 16)  // first bounce: pre-test rows by readlane, masked exact pass
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 8, true, true, 16, true, false>), g, b, psh, stream, q, q.sph);
-  else if (variant == 99 && tl && p.spp == 16)  // the same, pass 2 as a plain loop over the set bits
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 9, true, true, 16, true, false>), g, b, psh, stream, q, q.sph);
-  else if (variant == 95 && tl && p.spp == 16)  // first-bounce survivor loads waited together
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 5, true, true, 16, true, false>), g, b, psh, stream, q, q.sph);
-  else if (variant == 94 && tl && p.spp == 16)  // branchless hit tails in the later bounce rounds
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 4, true, true, 16, true, false>), g, b, psh, stream, q, q.sph);
   else if (variant == 93 && tl && p.spp == 16)  // section clocks of the production kernel
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true, 16, true>), g, b, psh, stream, q, q.sph);
   else if (variant == 93 && tl)
@@ -2181,7 +2113,6 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
   q.sph = p.shapes + sphere_table(p.S);
   q.planes = p.shapes + plane_table(p.S);
   q.b1_min = 1;
-  q.pool_ilv = 0;
   {  // rotation group: the pools of one image row (at least 8)
     const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
     const int ppr = p.W / TP;
@@ -2196,10 +2127,7 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
     const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
     const long long pools = (npix + TP - 1) / TP;
     const bool tl = p.nobj <= kTailMaxObj;
-    size_t psh = (size_t)batch_lds(p.spp, kPool, tl ? p.nobj : 0).total;
-#if RTRT_AB
-    if (const char* el = getenv("RTRT_LDS_EXTRA")) psh += (size_t)atoi(el);  // LDS allocation-granule probe
-#endif
+    const size_t psh = (size_t)batch_lds(p.spp, kPool, tl ? p.nobj : 0).total;
     const dim3 g((unsigned)pools), b(64);
     // timed launches pass no counters: the counter code is compiled out (fewer live scalars)
     const bool cnt = p.counters || p.row_counters;

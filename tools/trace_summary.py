@@ -44,7 +44,10 @@ def main():
             insts[inst] = insts[inst][:3] + (insts[inst][3] + 1,)
         for inst, (v, sg, lds, n) in insts.items():
             print(f"{key}: {inst}: {n} launches, vgpr={v} sgpr={sg} lds(static)={lds}")
-        print(f"  all={[round(d, 3) for d in ds]}")
+        if len(ds) <= 40:
+            print(f"  all={[round(d, 3) for d in ds]}")
+        else:  # long warm-up (bench.py settles the clock first): the launches after it
+            print(f"  {len(ds)} launches; after the {warm} warm-up: {[round(d, 3) for d in ds[warm:]]}")
         if timed:
             print(f"  timed mean={sum(timed) / len(timed):.4f} ms")
         solo = ds[warm + steps:warm + steps + 2]
