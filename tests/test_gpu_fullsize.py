@@ -28,9 +28,15 @@ PROGS = {1: [oracle.AOP_COMPUTE, oracle.AOP_POSTPROCESSING], 2: [oracle.AO_COMPU
          4: [oracle.H_COMPUTE]}
 
 
-def advance(h, mode: int, k: int, frame: int):
+def advance(h, mode: int, k: int, frame: int, moving: bool = False):
     """The render loop's per-frame host update (src/main.cpp:553-578): rand_buffer for the AO
-    modes, moving_light for the Phong modes; then mode.y = frame slot."""
+    modes, moving_light for the Phong modes; then mode.y = frame slot.  moving: the camera also
+    flies (a scripted path, as the keyboard camera of src/main.cpp:701-760 would move it)."""
+    if moving:
+        from real_time_ray_tracer_amd import aspect_for
+        a = 0.03 * k
+        h.camera_basis((0.5 * k, 0.1 * k, 14.0 - 0.5 * k), (0.0, 1.0, 0.0), (np.sin(a), -0.02 * k, np.cos(a)),
+                       aspect_for(*CONFIGS["d"][:2]))
     if mode in (1, 2):
         h.fill_rand_buffer(7000 + k)
     else:
@@ -38,7 +44,7 @@ def advance(h, mode: int, k: int, frame: int):
     h.set_mode(frame, h.num_objects)
 
 
-def gpu_render(cfg: str, frames: int, pipelined: bool = False) -> Renderer:
+def gpu_render(cfg: str, frames: int, pipelined: bool = False, moving: bool = False) -> Renderer:
     W, H, S, spp, mode, _ = CONFIGS[cfg]
     h = config_header(cfg)
     r = Renderer(W, H, S, spp)
@@ -46,14 +52,14 @@ def gpu_render(cfg: str, frames: int, pipelined: bool = False) -> Renderer:
         r.enable_pipelining(True)
     f = 0
     for k in range(frames):
-        advance(h, mode, k, f)
+        advance(h, mode, k, f, moving)
         r.upload_header(h)
         f = r.dispatch(mode, f)
     r.synchronize()
     return r
 
 
-def oracle_window(cfg: str, frames: int, x0: int, x1: int, y0: int, y1: int):
+def oracle_window(cfg: str, frames: int, x0: int, x1: int, y0: int, y1: int, moving: bool = False):
     """The oracle over columns [x0, x1) x rows [y0, y1) for the same frame sequence: image
     window [h][w][4] and the ring's window ([F][w][h][4] each: pixels, normals, depth)."""
     W, H, S, spp, mode, _ = CONFIGS[cfg]
@@ -67,7 +73,7 @@ def oracle_window(cfg: str, frames: int, x0: int, x1: int, y0: int, y1: int):
     nt = oracle.nthreads_default()
     f = 0
     for k in range(frames):
-        advance(h, mode, k, f)
+        advance(h, mode, k, f, moving)
         buf[:h.data.size] = h.data
         for p in PROGS[mode]:
             if p in (oracle.AOP_COMPUTE, oracle.AO_COMPUTE):  # g-buffer writers: the halo too
@@ -102,9 +108,10 @@ def pick_tiles(img: np.ndarray) -> dict:
     return tiles
 
 
-def check_window(r: Renderer, cfg: str, frames: int, x0: int, x1: int, y0: int, y1: int, what: str):
+def check_window(r: Renderer, cfg: str, frames: int, x0: int, x1: int, y0: int, y1: int, what: str,
+                 moving: bool = False):
     mode = CONFIGS[cfg][4]
-    want_img, (wp, wn, wd) = oracle_window(cfg, frames, x0, x1, y0, y1)
+    want_img, (wp, wn, wd) = oracle_window(cfg, frames, x0, x1, y0, y1, moving)
     g = r.download_rect(x0, x1, y0, y1)
     assert_close(g.image, want_img, f"{what} image")
     nf = min(frames, 8)
@@ -142,6 +149,21 @@ def test_full_size_tiles(cfg, frames, pipelined):
         tiles[f"odd{i}"] = (min(max(0, x - T // 2), W - T), min(max(0, y - T // 2), H - T))
     for name, (x0, y0) in tiles.items():
         check_window(r, cfg, frames, x0, x0 + T, y0, y0 + T, f"config {cfg} tile {name} at ({x0}, {y0})")
+    r.close()
+
+
+def test_full_size_tiles_moving_camera():
+    """Config (d), pipelined, 10 frames with the camera flying: the temporal filter rejects
+    history where the scene moved, at 4K pixel coordinates; the same tile choice as above."""
+    r = gpu_render("d", 10, pipelined=True, moving=True)
+    img = r.image()
+    tiles = pick_tiles(img)
+    W, H = CONFIGS["d"][:2]
+    for i, (x, y) in enumerate(whole_frame_properties(img, "d")):
+        tiles[f"odd{i}"] = (min(max(0, x - T // 2), W - T), min(max(0, y - T // 2), H - T))
+    for name, (x0, y0) in tiles.items():
+        check_window(r, "d", 10, x0, x0 + T, y0, y0 + T, f"config d (moving camera) tile {name} at ({x0}, {y0})",
+                     moving=True)
     r.close()
 
 

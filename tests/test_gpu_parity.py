@@ -174,6 +174,52 @@ def test_mode1_long_sequence_ring_wraps():
     assert_bitwise(g.normals, s.normals, "normals ring")
 
 
+def camera_path(k: int):
+    """A scripted fly-through (what the reference's keyboard camera does each frame,
+    src/main.cpp:701-760): the camera moves forward and sideways and turns a little each frame."""
+    a = 0.05 * k
+    loc = (0.6 * np.sin(a) * k, 0.15 * k, 14.0 - 0.7 * k)
+    look = (np.sin(a), -0.04 * k, np.cos(a))  # look_towards (w); the basis normalizes u and v
+    return loc, (0.0, 1.0, 0.0), look
+
+
+@pytest.mark.parametrize("mode,pipelined", [(1, False), (1, True), (2, False), (3, False), (4, False)])
+def test_moving_camera_parity(mode, pipelined):
+    """The camera basis (render(), src/main.cpp:772-779) changes every frame: the pool and tile
+    cones follow it, and in mode 1 the temporal filter (aop_postprocessing.glsl:177-201) now
+    rejects history wherever the scene moved across the pixel.  11 frames (the ring wraps)."""
+    W, H, spp = 64, 48, 4
+    h = make_header("syn16p", W, H, spp)
+    r = Renderer(W, H, h.S, h.AA)
+    if pipelined:
+        r.enable_pipelining(True)
+    ho = h.copy()
+    s = SSBO(ho, W, H)
+    d = oracle.dims(W, H, h.S, h.AA)
+    img = np.zeros((H, W, 4), np.float32)
+    fg = fo = 0
+    for k in range(11):
+        for hh in (h, ho):
+            hh.camera_basis(*camera_path(k), aspect_for(W, H))
+            if mode in (1, 2):
+                hh.fill_rand_buffer(7000 + k)
+            else:
+                hh.moving_light(True)
+        h.set_mode(fg, h.num_objects)
+        r.upload_header(h)
+        fg = r.dispatch(mode, fg)
+        ho.set_mode(fo, ho.num_objects)
+        s.set_header(ho)
+        fo = oracle.dispatch(s.data, d, mode, fo, img)
+        assert fg == fo
+    g = r.download()
+    r.close()
+    assert_close(g.image, img, f"mode {mode} image")
+    assert_close(g.pixels, s.pixels, f"mode {mode} pixels ring")
+    assert_bitwise(g.normals, s.normals, f"mode {mode} normals ring")
+    assert_bitwise(g.depth, s.depth, f"mode {mode} depth ring")
+
+
 def test_mode_switching_shares_the_ring():
     """compute() keeps one static frame counter across modes (src/main.cpp:555)."""
     W, H = 40, 30
