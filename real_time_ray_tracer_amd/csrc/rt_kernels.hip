@@ -140,6 +140,24 @@ __device__ __forceinline__ void store_color(const FrameParams& P, int x, int y, 
 
 // The frame a Phong/hybrid block renders: its light, colour slot and image (multi-frame
 // launches: frame blockIdx.z of the batch, see FrameParams::mf_n).
+// Depth g-buffer slot layout: two planes of [band_rows][W] float2, (x, y) then (z, w).  The
+// post-process reads only depth.x and depth.y (aop_postprocessing.glsl: the neighbour weights and
+// the history test), so it reads 8 B per depth instead of 16; the AO pass writes both planes and
+// reads both for its stale-depth pixels.  rt_download / rt_upload_gbuffer convert to the
+// reference's vec4 layout.
+__device__ __forceinline__ size_t dep_plane(const FrameParams& P) { return (size_t)P.band_rows * P.W; }
+__device__ __forceinline__ void dep_store(float4* base, size_t n, size_t off, float4 d) {
+  float2* p = (float2*)base;
+  p[off] = make_float2(d.x, d.y);
+  p[n + off] = make_float2(d.z, d.w);
+}
+__device__ __forceinline__ float4 dep_load(const float4* base, size_t n, size_t off) {
+  const float2* p = (const float2*)base;
+  const float2 a = p[off], b = p[n + off];
+  return make_float4(a.x, a.y, b.x, b.y);
+}
+__device__ __forceinline__ float2 dep_load_xy(const float4* base, size_t off) { return ((const float2*)base)[off]; }
+
 struct FrameDst {
   f3 light;
   float4* out_pix;
@@ -888,12 +906,12 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4*
   } else {
     // stale: sample 0 hit an emissive shape first (no g-buffer write): the slot keeps its
     // previous normal and depth (read from the slot's previous buffers when pipelined)
-    d = P.dep_prev[off];
+    d = dep_load(P.dep_prev, dep_plane(P), off);
     if (P.nrm_prev != P.nrm) P.nrm[off] = P.nrm_prev[off];
   }
   if (ystop >= 0.0f) d.y = ystop;
   d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
-  P.dep[off] = d;
+  dep_store(P.dep, dep_plane(P), off, d);
   store_color(P, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
 }
 
@@ -1062,7 +1080,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       pool_xy(lp, x, y);
       const size_t off = (size_t)(y - P.band_row0) * W + x;
       f_nrm[off] = z;
-      f_dep[off] = z;  // (0, 0, 0, 0) / AA
+      dep_store(f_dep, dep_plane(P), off, z);  // (0, 0, 0, 0) / AA
       store_color(P, f_out, f_img, x, y, col);
       if (rowc) atomicAdd(&rowc[y - P.band_row0], (unsigned long long)spp);  // ~free
     }
@@ -1460,12 +1478,12 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       f_nrm[off] = d;
     } else {  // stale: the slot's previous normal / depth (an emissive first hit writes neither)
-      d = f_dep_prev[off];
+      d = dep_load(f_dep_prev, dep_plane(P), off);
       if (f_nrm_prev != f_nrm) f_nrm[off] = f_nrm_prev[off];
     }
     if (ystop >= 0.0f) d.y = ystop;
     d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
-    f_dep[off] = d;
+    dep_store(f_dep, dep_plane(P), off, d);
     store_color(P, f_out, f_img, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
   }
   if ((kLaps || ABL == 7) && cnts && lane == 0) {
@@ -1586,7 +1604,7 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
         pool_xy(lp, x, y);
         const size_t off = (size_t)(y - P.band_row0) * W + x;
         P.nrm[off] = z;
-        P.dep[off] = z;
+        dep_store(P.dep, dep_plane(P), off, z);
         store_color(P, x, y, c);
         if (P.row_counters) atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)spp);
       }
@@ -1629,12 +1647,12 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
           d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
           P.nrm[off] = d;
         } else {  // stale (see ao_kernel)
-          d = P.dep_prev[off];
+          d = dep_load(P.dep_prev, dep_plane(P), off);
           if (P.nrm_prev != P.nrm) P.nrm[off] = P.nrm_prev[off];
         }
         if (ystop >= 0.0f) d.y = ystop;
         d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
-        P.dep[off] = d;
+        dep_store(P.dep, dep_plane(P), off, d);
         store_color(P, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
         pstop[s * TPs + lq] = -1;
       }
@@ -1850,7 +1868,7 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, unsigned& visited, unsigned& accepted);
 
-__device__ __forceinline__ float nbr_weight(f3 n, float nd, float nb, float4 kn, float4 kd) {
+__device__ __forceinline__ float nbr_weight(f3 n, float nd, float nb, float4 kn, float2 kd) {
   if (kn.w < 0.001f) return 1.0f;
   float normal_dot = dot(n, xyz(kn));
   float depth_diff = 1.0f - gclamp(fabsf(nd - kd.x), 0.0f, 1.0f);
@@ -1882,7 +1900,7 @@ __device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, u
   float4 color = P.raw[off];
   const float4 cn = P.nrm[off];
   if (cn.w > 0.99f) {
-    const float4 cd = P.dep[off];
+    const float2 cd = dep_load_xy(P.dep, off);
     const f3 nv = xyz(cn);
     const float nd = cd.x, nb = cd.y;
     float4 acc = color;
@@ -1899,7 +1917,7 @@ __device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, u
       float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       if (present) {
         size_t o = (size_t)(yy - P.band_row0) * W + xx;
-        wk = nbr_weight(nv, nd, nb, P.nrm[o], P.dep[o]);
+        wk = nbr_weight(nv, nd, nb, P.nrm[o], dep_load_xy(P.dep, o));
         v = P.raw[o];
       }
       acc.x = acc.x + wk * v.x; acc.y = acc.y + wk * v.y;
@@ -1913,7 +1931,7 @@ __device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, u
     for (int i = 1; i < P.F; ++i) {
       int cf = (f + P.F - i) % P.F;
       float4 hn = P.hist_nrm[cf][off];
-      float4 hd = P.hist_dep[cf][off];
+      const float2 hd = dep_load_xy(P.hist_dep[cf], off);
       float normal_dot = dot(nv, xyz(hn));
       float depth_diff = 1.0f - gclamp(fabsf(nd - hd.x), 0.0f, 1.0f);
       float bounces_diff = 1.0f - gclamp(fabsf(nb - hd.y) / 1.7f, 0.0f, 1.0f);

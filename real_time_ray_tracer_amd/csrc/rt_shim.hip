@@ -455,6 +455,25 @@ int resolve_timing(rt_ctx* c) {
   return RT_OK;
 }
 
+// Depth slots are two planes of [band_rows][W] float2, (x, y) then (z, w) (rt_kernels.hip
+// dep_store): converted to / from interleaved [band_rows][W] float4 around the copies.
+void depth_planes_to_vec4(const float* planes, size_t n, float* v) {
+  for (size_t i = 0; i < n; ++i) {
+    v[4 * i + 0] = planes[2 * i];
+    v[4 * i + 1] = planes[2 * i + 1];
+    v[4 * i + 2] = planes[2 * (n + i)];
+    v[4 * i + 3] = planes[2 * (n + i) + 1];
+  }
+}
+void depth_vec4_to_planes(const float* v, size_t n, float* planes) {
+  for (size_t i = 0; i < n; ++i) {
+    planes[2 * i] = v[4 * i + 0];
+    planes[2 * i + 1] = v[4 * i + 1];
+    planes[2 * (n + i)] = v[4 * i + 2];
+    planes[2 * (n + i) + 1] = v[4 * i + 3];
+  }
+}
+
 // device slot [band_rows][W] float4 (own rows) <-> reference [W][R] vec4
 void dev_to_ref(const rt_ctx* c, const float* slot, float* ref) {
   const int W = c->cfg.width, R = c->own_rows, r0 = c->own0 - c->band0;
@@ -905,7 +924,7 @@ int rt_download(rt_ctx* c, float* pixels, float* normals, float* depth, float* i
   const int F = c->cfg.num_frames;
   const size_t slot = slot_elems(c);
   const size_t ref_slot = (size_t)c->cfg.width * c->own_rows * 4;
-  std::vector<float> tmp(slot * 4);
+  std::vector<float> tmp(slot * 4), tmp2(depth ? slot * 4 : 0);
   int rc = join(c);
   if (rc == RT_OK) rc = sync_all(c);
   if (rc != RT_OK) return rc;
@@ -919,7 +938,8 @@ int rt_download(rt_ctx* c, float* pixels, float* normals, float* depth, float* i
       dev_to_ref(c, tmp.data(), normals + f * ref_slot);
     }
     if (depth) {
-      RT_HIP(c, hipMemcpy(tmp.data(), c->dep[c->dep_slot[f]], slot * 16, hipMemcpyDeviceToHost));
+      RT_HIP(c, hipMemcpy(tmp2.data(), c->dep[c->dep_slot[f]], slot * 16, hipMemcpyDeviceToHost));
+      depth_planes_to_vec4(tmp2.data(), slot, tmp.data());
       dev_to_ref(c, tmp.data(), depth + f * ref_slot);
     }
   }
@@ -943,12 +963,23 @@ int rt_download_rect(rt_ctx* c, int x0, int x1, int y0, int y1, float* pixels, f
   auto rect = [&](const float4* base, int r0) {  // rows [r0, r0 + h) of a [rows][W] device array
     return hipMemcpy2D(tmp.data(), row, base + (size_t)r0 * W + x0, pitch, row, h, hipMemcpyDeviceToHost);
   };
+  // a depth slot's rect: the (x, y) and (z, w) planes, interleaved into tmp
+  const size_t n = slot_elems(c), pitch2 = (size_t)W * sizeof(float2), row2 = (size_t)w * sizeof(float2);
+  std::vector<float2> t0((size_t)w * h), t1((size_t)w * h);
+  auto depth_rect = [&](const float4* base, int r0) -> hipError_t {
+    const float2* p = (const float2*)base + (size_t)r0 * W + x0;
+    hipError_t e = hipMemcpy2D(t0.data(), row2, p, pitch2, row2, h, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy2D(t1.data(), row2, p + n, pitch2, row2, h, hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < t0.size(); ++i) tmp[i] = make_float4(t0[i].x, t0[i].y, t1[i].x, t1[i].y);
+    return e;
+  };
   for (int f = 0; f < F; ++f) {
     struct { float* dst; const float4* src; } items[3] = {
         {pixels, c->pix[c->pix_slot[f]]}, {normals, c->nrm[c->nrm_slot[f]]}, {depth, c->dep[c->dep_slot[f]]}};
-    for (auto& it : items) {
+    for (int k = 0; k < 3; ++k) {
+      auto& it = items[k];
       if (!it.dst) continue;
-      RT_HIP(c, rect(it.src, y0 - c->band0));
+      RT_HIP(c, k == 2 ? depth_rect(it.src, y0 - c->band0) : rect(it.src, y0 - c->band0));
       float* out = it.dst + (size_t)f * w * h * 4;  // [w][h] vec4, y fastest (reference layout)
       for (int x = 0; x < w; ++x)
         for (int r = 0; r < h; ++r) std::memcpy(out + ((size_t)x * h + r) * 4, &tmp[(size_t)r * w + x], 16);
@@ -967,18 +998,22 @@ int rt_upload_gbuffer(rt_ctx* c, const float* pixels, const float* normals, cons
   const int F = c->cfg.num_frames;
   const size_t slot = slot_elems(c);
   const size_t ref_slot = (size_t)c->cfg.width * c->own_rows * 4;
-  std::vector<float> tmp(slot * 4);
+  std::vector<float> tmp(slot * 4), tmp2(depth ? slot * 4 : 0);
   int rc = join(c);
   if (rc == RT_OK) rc = sync_all(c);
   if (rc != RT_OK) return rc;
   for (int f = 0; f < F; ++f) {
     struct { const float* src; float4* dst; } items[3] = {
         {pixels, c->pix[c->pix_slot[f]]}, {normals, c->nrm[c->nrm_slot[f]]}, {depth, c->dep[c->dep_slot[f]]}};
-    for (auto& it : items) {
+    for (int k = 0; k < 3; ++k) {
+      auto& it = items[k];
       if (!it.src) continue;
-      RT_HIP(c, hipMemcpy(tmp.data(), it.dst, slot * 16, hipMemcpyDeviceToHost));  // keep halo rows
+      const bool dp = k == 2;  // depth slots hold two float2 planes
+      RT_HIP(c, hipMemcpy(dp ? tmp2.data() : tmp.data(), it.dst, slot * 16, hipMemcpyDeviceToHost));  // keep halo rows
+      if (dp) depth_planes_to_vec4(tmp2.data(), slot, tmp.data());
       ref_to_dev(c, it.src + f * ref_slot, tmp.data());
-      RT_HIP(c, hipMemcpy(it.dst, tmp.data(), slot * 16, hipMemcpyHostToDevice));
+      if (dp) depth_vec4_to_planes(tmp.data(), slot, tmp2.data());
+      RT_HIP(c, hipMemcpy(it.dst, dp ? tmp2.data() : tmp.data(), slot * 16, hipMemcpyHostToDevice));
     }
   }
   return RT_OK;
