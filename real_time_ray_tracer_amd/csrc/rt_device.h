@@ -278,6 +278,14 @@ __device__ __forceinline__ void sphere_candidate(f3 pos, f3 dir, float4 g, int i
   }
 }
 
+// The lowest set bit of a wave-uniform 64-bit mask, cleared with one s_bitset0_b64 (the
+// compiler's m & (m - 1) is a 64-bit subtract and an and: three scalar instructions).
+__device__ __forceinline__ int pop_lowest(unsigned long long& m) {
+  const int j = __builtin_ctzll(m);
+  asm("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(j));
+  return j;
+}
+
 // One plane of the min-t scan, tested out of index order (after the spheres): plane_eval_ray
 // (p_compute.glsl:111-119) and the scan's acceptance, with the tie rule made explicit.  The
 // sequential scan (`res > thr && (res < t || t < 0)`, ascending i) ends with the accepted

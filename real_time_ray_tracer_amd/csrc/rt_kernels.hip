@@ -1218,8 +1218,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
             (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
         while (m) {
-          int i = (w << 6) + __builtin_ctzll(m);
-          m &= m - 1;
+          const int i = (w << 6) + pop_lowest(m);
           sphere_candidate(bpos, bdir, geo[i], i, 0.0001f, t, ind);
           if (ABL == 2) {  // timing ablation: the culled primary tests twice
             float z;
@@ -1273,8 +1272,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
             if (ABL == 6) lap(5);
             if (live)
               while (m) {
-                const int k = (w << 6) + __builtin_ctzll(m);
-                m &= m - 1;
+                const int k = (w << 6) + pop_lowest(m);
                 const float4 q = geol[k];  // wave-uniform address: LDS broadcast
                 const float4 g = geo[k];
                 if (ABL == 7) {  // survivor iterations; with any pre-test pass; with any del >= 0 there
@@ -1752,8 +1750,7 @@ __global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, cons
         m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
             (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
         while (m) {
-          int i = (w << 6) + __builtin_ctzll(m);
-          m &= m - 1;
+          const int i = (w << 6) + pop_lowest(m);
           sphere_candidate(bpos, bdir, geo[i], i, 0.0001f, t, ind);
         }
       }
