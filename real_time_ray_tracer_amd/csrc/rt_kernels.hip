@@ -1270,11 +1270,13 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
             geol_valid = false;
             __syncthreads();  // the pre-test rows are written
             if (ABL == 6) lap(5);
+            const float4* const qw = geol + (w << 6);  // this word's rows and spheres (fewer
+            const float4* const gw = geo + (w << 6);   // scalar address operations per survivor)
             if (live)
               while (m) {
-                const int k = (w << 6) + pop_lowest(m);
-                const float4 q = geol[k];  // wave-uniform address: LDS broadcast
-                const float4 g = geo[k];
+                const int j = pop_lowest(m), k = (w << 6) + j;
+                const float4 q = qw[j];  // wave-uniform address: LDS broadcast
+                const float4 g = gw[j];
                 if (ABL == 7) {  // survivor iterations; with any pre-test pass; with any del >= 0 there
                   const bool pass = fmaf(bdir.z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w;
                   const f3 pmc = bpos - xyz(g);
