@@ -1272,10 +1272,21 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
             if (ABL == 6) lap(5);
             const float4* const qw = geol + (w << 6);  // this word's rows and spheres (fewer
             const float4* const gw = geo + (w << 6);   // scalar address operations per survivor)
+            // the row's LDS address is formed by one vector instruction from the row base held in
+            // a VGPR (the compiler builds the uniform address with two scalar instructions and
+            // copies it to a VGPR), and the broadcast read waits at once, as the loop would
+            int qbase;
+            asm("v_mov_b32 %0, %1" : "=v"(qbase) : "s"((int)(size_t)((const char*)qw - lbase)));
             if (live)
               while (m) {
                 const int j = pop_lowest(m), k = (w << 6) + j;
-                const float4 q = qw[j];  // wave-uniform address: LDS broadcast
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                v4f qv;
+                int j_addr_scratch;
+                asm volatile("v_lshl_add_u32 %1, %2, 4, %3\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                             : "=v"(qv), "=&v"(j_addr_scratch)
+                             : "s"(j), "v"(qbase));
+                const float4 q = make_float4(qv.x, qv.y, qv.z, qv.w);  // wave-uniform address: LDS broadcast
                 const float4 g = gw[j];
                 if (ABL == 7) {  // survivor iterations; with any pre-test pass; with any del >= 0 there
                   const bool pass = fmaf(bdir.z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w;
