@@ -351,36 +351,6 @@ __device__ __forceinline__ int closest_hit_pf(const float4* __restrict__ geo, in
   return ind;
 }
 
-// closest_hit_pf with its group loop unrolled U times (fewer scalar loop instructions per
-// sphere; same visiting order and acceptance)
-template <int U>
-__device__ __forceinline__ int closest_hit_pf_u(const float4* __restrict__ geo, int nobj, f3 pos, f3 dir, float thr,
-                                                float& t_out) {
-  float t = -1.0f;
-  int ind = -1;
-  int i = 0;
-  if (nobj >= 4) {
-    float4 g0 = geo[0], g1 = geo[1], g2 = geo[2], g3 = geo[3];
-#pragma unroll U
-    for (; i + 8 <= nobj; i += 4) {
-      float4 n0 = geo[i + 4], n1 = geo[i + 5], n2 = geo[i + 6], n3 = geo[i + 7];
-      sphere_candidate(pos, dir, g0, i, thr, t, ind);
-      sphere_candidate(pos, dir, g1, i + 1, thr, t, ind);
-      sphere_candidate(pos, dir, g2, i + 2, thr, t, ind);
-      sphere_candidate(pos, dir, g3, i + 3, thr, t, ind);
-      g0 = n0; g1 = n1; g2 = n2; g3 = n3;
-    }
-    sphere_candidate(pos, dir, g0, i, thr, t, ind);
-    sphere_candidate(pos, dir, g1, i + 1, thr, t, ind);
-    sphere_candidate(pos, dir, g2, i + 2, thr, t, ind);
-    sphere_candidate(pos, dir, g3, i + 3, thr, t, ind);
-    i += 4;
-  }
-  for (; i < nobj; ++i) sphere_candidate(pos, dir, geo[i], i, thr, t, ind);
-  t_out = t;
-  return ind;
-}
-
 // closest_hit_pf over the n <= 64 spheres geo[0..n) (indices base + i) whose bit is set in the
 // wave-uniform mask m: the table is still streamed 4 spheres per scalar load, prefetched one
 // group ahead, and a sphere whose bit is clear is skipped by a scalar branch.  Ascending order

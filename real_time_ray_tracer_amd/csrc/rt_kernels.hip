@@ -1424,8 +1424,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     }
     if (has) {
       float t;
-      // 4-sphere scalar groups (pf2: +0.9%), the group loop unrolled 4x (-1.1% (d), -2.1% (c))
-      int ind = closest_hit_pf_u<4>(geo, nobj, pos, dir, 0.0001f, t);
+      int ind = closest_hit_pf(geo, nobj, pos, dir, 0.0001f, t);  // 4-sphere scalar groups (pf2: +0.9%)
       if (PL) plane_pass(P, pos, dir, 0.0001f, t, ind);
       if (ABL == 1) {  // timing ablation: the bounce tests twice
         float z, t2;
