@@ -1504,372 +1504,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   }
 }
 
-#if RTRT_AB  // the streaming AO kernel (rejected): A/B builds only
-// ---------------------------------------------------------------------------------------
-// Streaming AO (all-sphere scenes).  The pooled kernel above loses ~25% of its bounce-round
-// lane slots at the end of each pool, when the last long paths run with most lanes idle.
-// Here one wave streams through K consecutive sub-pools (SUB samples each: SUB/spp pixels x
-// spp) and keeps preparing new samples while the previous sub-pools' long paths finish: the
-// per-sample results live in a ring of R sub-pool slots in LDS, and a sub-pool is combined
-// (in sample order, as ao_compute.glsl:303-339) as soon as all its samples are done.  Same
-// per-sample arithmetic, culling, shading and combine as ao_batch_kernel (bit-identical).
-// ---------------------------------------------------------------------------------------
-__host__ __device__ constexpr size_t stream_lds_bytes(int spp, int nobj, int SUB, int R, int K) {
-  return (size_t)R * (SUB / spp > 0 ? SUB / spp : 1) * (16 + 4 + 4) +            // prec, pstop, pkind
-         (size_t)3 * R * (SUB / spp > 0 ? SUB / spp : 1) * spp * 4 +              // sres
-         (size_t)R * 4 + (size_t)K * 4 + 64 * 4 + 8 +                             // sdone, sncull, perm
-         (size_t)K * ((nobj + 63) / 64) * 8 + 16 + (size_t)2 * spp * 16;          // cmask, rls
-}
-
-template <int MINW, int SUB, int R, int CG = 2>
-__global__ __launch_bounds__(64, MINW) void ao_stream_kernel(FrameParams P, const float4* __restrict__ geo, int K,
-                                                             float inv_tps) {
-  extern __shared__ float4 lds[];
-  const int spp = P.spp, W = P.W, D = P.D, nobj = P.nobj;
-  const int TPs = SUB / spp > 0 ? SUB / spp : 1;  // pixels per sub-pool
-  const int SUBN = TPs * spp;                      // samples per sub-pool
-  const int lane = threadIdx.x;
-  const int nwords = (nobj + 63) >> 6;
-  float4* prec = lds;                              // [R*TPs] first-segment (normal, t) of sample 0
-  float* sres = (float*)(prec + R * TPs);          // [3][R*SUBN] per-sample r, g, b
-  int* pstop = (int*)(sres + 3 * R * SUBN);        // [R*TPs] max (aa << 16 | stop value)
-  int* pkind = pstop + R * TPs;                    // [R*TPs]
-  int* sdone = pkind + R * TPs;                    // [R] finished samples of the slot's sub-pool
-  int* sncull = sdone + R;                         // [K] culled-set size per sub-pool (-1: empty frustum)
-  int* perm = sncull + K;                          // [64] live-rank -> lane of the prepared batch
-  unsigned long long* cmask = (unsigned long long*)(((uintptr_t)(perm + 64) + 7) & ~(uintptr_t)7);  // [K][nwords]
-  float4* rls = (float4*)(((uintptr_t)(cmask + K * nwords) + 15) & ~(uintptr_t)15);                // [2*spp]
-  for (int k = lane; k < 2 * spp; k += 64) rls[k] = P.rb[k];
-  for (int k = lane; k < R * TPs; k += 64) pstop[k] = -1;
-  if (lane < R) sdone[lane] = 0;
-  const float4* col = P.shapes + 2 * P.S;
-  const float4* aux = P.shapes + 3 * P.S;
-  const float4* rbuf = rls;
-
-  const long long npix = (long long)P.trace_rows * W;
-  const int TPw = K * TPs;
-  const long long p0 = (long long)blockIdx.x * TPw;
-  const int npw = (int)(npix - p0 < TPw ? npix - p0 : TPw);
-  const int totalw = npw * spp;
-  const int yf = P.trace_row0 + (int)(p0 / W), xf = (int)(p0 % W);  // once per wave (scalar)
-  auto pool_xy = [&](int lp, int& x, int& y) {  // wave-local pixel -> (x, y)
-    int xi = xf + lp;
-    y = yf;
-    if (xi >= W) {
-      int q = (int)((unsigned)xi / (unsigned)W);
-      y += q;
-      xi -= q * W;
-    }
-    x = xi;
-  };
-  const float inv_spp = P.inv_spp;
-  // exact small-integer quotients via float reciprocals (operands < 2^16, error << 0.5/divisor)
-  auto div_spp = [&](int it) { return (int)(((float)it + 0.5f) * inv_spp); };
-  auto div_tps = [&](int lp) { return (int)(((float)lp + 0.5f) * inv_tps); };
-  auto sub_count = [&](int j) { return ((j + 1) * TPs < npw ? TPs : npw - j * TPs) * spp; };
-  __syncthreads();
-
-  const f3 cam = mk(P.cx, P.cy, P.cz);
-  bool has = false;
-  int item = 0, depth = 0;
-  f3 pos = cam, dir = cam, hemi = cam;
-  float rr = 1.0f, rg = 1.0f, rb = 1.0f;
-  int bitem = 0;
-  f3 bpos = cam, bdir = cam, bhemi = cam;
-  float br = 1.0f, bg = 1.0f, bb = 1.0f;
-  int next = 0, cursor = 0, nlive = 0, jcomb = 0, jcull = -1;  // wave-uniform
-  unsigned nseg = 0;
-  unsigned long long exec_tests = 0, fast_samples = 0;
-
-  // ---- sub-pool j: frustum cull (and the empty-frustum fast path) -------------------------
-  // cone cull of sub-pools [j0, j1) together (one cone over their pixels; a superset of each
-  // sub-pool's own cone, so still conservative), and the empty-frustum fast path
-  auto cull = [&](int j0, int j1) {
-    const int a = j0 * TPs, e = j1 * TPs < npw ? j1 * TPs : npw;
-    int xa, ya, xe, ye;
-    pool_xy(a, xa, ya);
-    pool_xy(e - 1, xe, ye);
-    const ConeF cone = pool_cone_f(P, ya == ye ? xa : 0, ya == ye ? xe : W - 1, ya, ye);
-    int nc = 0;
-    for (int w = 0; w < nwords; ++w) {
-      int i = (w << 6) + lane;
-      bool keep = i < nobj && !cone_misses_f(cone, geo[i], P.cx, P.cy, P.cz);
-      unsigned long long m = __ballot(keep);
-      nc += __popcll(m);
-      if (lane == 0)
-        for (int j = j0; j < j1; ++j) cmask[j * nwords + w] = m;
-    }
-    const bool fast = nc == 0;
-    if (lane == 0)
-      for (int j = j0; j < j1; ++j) sncull[j] = fast ? -1 : nc;
-    if (fast) {  // every primary ray misses every sphere: as ao_batch_kernel's fast path
-      const float fa = (float)spp;
-      float sr = 0.0f, sg = 0.0f, sb = 0.0f;
-      for (int k = 0; k < spp; ++k) {
-        sr = sr + 1.0f * P.bg.x; sg = sg + 1.0f * P.bg.y; sb = sb + 1.0f * P.bg.z;
-      }
-      const float4 c = gamma_out(sr / fa, sg / fa, sb / fa);
-      const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      for (int lp = a + lane; lp < e; lp += 64) {
-        int x, y;
-        pool_xy(lp, x, y);
-        const size_t off = (size_t)(y - P.band_row0) * W + x;
-        P.nrm[off] = z;
-        dep_store(P.dep, dep_plane(P), off, z);
-        store_color(P, x, y, c);
-        if (P.row_counters) atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)spp);
-      }
-      for (int j = j0; j < j1; ++j) fast_samples += (unsigned long long)sub_count(j);
-    }
-  };
-  // every sub-pool's cull up front (and the empty ones written), before any path is live
-  {
-    const int nsub = (npw + TPs - 1) / TPs;
-    const int cg = CG > 0 ? CG : 1;  // sub-pools per cone
-    for (int j = 0; j < nsub; j += cg) cull(j, j + cg < nsub ? j + cg : nsub);
-    __syncthreads();
-  }
-
-  // ---- sub-pool j: combine in sample order and free its slot -----------------------------
-  auto combine = [&](int j) {
-    const int s = j % R;
-    if (__builtin_amdgcn_readfirstlane(sncull[j]) >= 0) {
-      const int a = j * TPs, e = (j + 1) * TPs < npw ? (j + 1) * TPs : npw;
-      const float* base = sres + s * SUBN;
-      for (int lq = lane; lq < e - a; lq += 64) {
-        int x, y;
-        pool_xy(a + lq, x, y);
-        float sr = 0.0f, sg = 0.0f, sb = 0.0f;
-        const float* ps = base + lq * spp;
-        for (int k = 0; k < spp; ++k) {
-          sr = sr + ps[k]; sg = sg + ps[R * SUBN + k]; sb = sb + ps[2 * R * SUBN + k];
-        }
-        const int st = pstop[s * TPs + lq];
-        const float ystop = st < 0 ? -1.0f : (float)(st & 0xffff);
-        const float fa = (float)spp;
-        const size_t off = (size_t)(y - P.band_row0) * W + x;
-        const int kind = pkind[s * TPs + lq];
-        float4 d;
-        if (kind == PRIM_HIT) {
-          float4 r0 = prec[s * TPs + lq];
-          d = make_float4(r0.w, 0.0f, 0.0f, 1.0f);
-          P.nrm[off] = make_float4(r0.x, r0.y, r0.z, 1.0f);
-        } else if (kind == PRIM_MISS) {
-          d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          P.nrm[off] = d;
-        } else {  // stale (see ao_kernel)
-          d = dep_load(P.dep_prev, dep_plane(P), off);
-          if (P.nrm_prev != P.nrm) P.nrm[off] = P.nrm_prev[off];
-        }
-        if (ystop >= 0.0f) d.y = ystop;
-        d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
-        dep_store(P.dep, dep_plane(P), off, d);
-        store_color(P, x, y, gamma_out(sr / fa, sg / fa, sb / fa));
-        pstop[s * TPs + lq] = -1;
-      }
-    }
-    if (lane == 0) sdone[s] = 0;
-    __syncthreads();
-  };
-
-  auto finish = [&](int it, float r, float g, float b, float stopv, int segs) {
-    const int lp = div_spp(it), j = div_tps(lp), s = j % R;
-    const int k = s * SUBN + (it - j * SUBN);
-    sres[k] = r;
-    sres[R * SUBN + k] = g;
-    sres[2 * R * SUBN + k] = b;
-    if (stopv >= 0.0f) atomicMax(&pstop[s * TPs + (lp - j * TPs)], ((it - lp * spp) << 16) | (int)stopv);
-    if (P.row_counters) {
-      int x, y;
-      pool_xy(lp, x, y);
-      atomicAdd(&P.row_counters[y - P.band_row0], (unsigned long long)(kSetupCost + sncull[j] + (segs - 1) * nobj));
-    }
-  };
-
-  auto shade = [&](int ind, float t, f3& ps, f3& dr, f3 hm, float& r, float& g, float& b, int dpt, int it,
-                   bool first) -> bool {
-    const int lp = div_spp(it), aa = it - lp * spp;
-    const int j = div_tps(lp), q = (j % R) * TPs + (lp - j * TPs);
-    if (ind != -1) {
-      float4 att = col[ind];
-      float4 ax = aux[ind];
-      if (ax.x > 0.9f) {
-        r = r * att.x; g = g * att.y; b = b * att.z;
-        if (aa == 0 && first) pkind[q] = PRIM_EMISSIVE;
-        finish(it, r, g, b, (float)(D - dpt), D - dpt + 1);
-        return false;
-      }
-      f3 curr = cam + t * dr;  // sic: camera origin (ao_compute.glsl:210)
-      f3 nn = normalize(curr - xyz(geo[ind]));
-      if (aa == 0 && first) {
-        pkind[q] = PRIM_HIT;
-        prec[q] = make_float4(nn.x, nn.y, nn.z, t);
-      }
-      r = r * att.x; g = g * att.y; b = b * att.z;
-      ps = curr;
-      float reflect = ax.y;
-      if (reflect > 0.999f) {
-        dr = normalize(hm + nn);
-      } else {
-        float dn = dot(dr, nn);
-        f3 Rv = normalize(mk(dr.x - 2.0f * (dn * nn.x), dr.y - 2.0f * (dn * nn.y), dr.z - 2.0f * (dn * nn.z)));
-        dr = normalize(Rv + reflect * hm);
-      }
-      if (dpt - 1 == 0) {
-        finish(it, r, g, b, -1.0f, D);
-        return false;
-      }
-      return true;
-    }
-    if (aa == 0 && first) pkind[q] = PRIM_MISS;
-    r = r * P.bg.x; g = g * P.bg.y; b = b * P.bg.z;
-    finish(it, r, g, b, (float)(D - dpt), D - dpt + 1);
-    return false;
-  };
-
-  // Prepare up to 64 samples of sub-pool j = next / SUBN (never straddling a sub-pool).
-  auto prepare = [&](int j) {
-    const int s = j % R;
-    const int jend = (j + 1) * SUBN < totalw ? (j + 1) * SUBN : totalw;
-    const int bend = next + 64 < jend ? next + 64 : jend;
-    const int ncull = __builtin_amdgcn_readfirstlane(sncull[j]);
-    bitem = next + lane;
-    bool live = false;
-    exec_tests += (unsigned long long)ncull;
-    if (bitem < bend) {
-      const int lp = div_spp(bitem), aa = bitem - lp * spp;
-      int x, y;
-      pool_xy(lp, x, y);
-      const float px = (float)x, py = (float)y;
-      float hp, vp;
-      {  // ao_compute.glsl:310-323; sample 0 is unjittered: px + 0 == px, so one path for
-        // every lane (no divergent branch in the batch)
-        float4 f = rbuf[2 * aa], sv = rbuf[2 * aa + 1];
-        float u = grandom(((sv.x + px * f.z) - px) + f.x, ((f.y + py * sv.w) - py) + sv.y);
-        float w = grandom(sv.z * px - (f.x * px) * f.z, f.w * py - (sv.y * py) * sv.w);
-        normalize2(u, w);
-        const float jx = aa == 0 ? 0.0f : div_rn_by(u, 6.0f, kInv6) - 0.08333f;
-        const float jy = aa == 0 ? 0.0f : div_rn_by(w, 6.0f, kInv6) - 0.08333f;
-        hp = div_rn_by(px + jx, P.fW, P.inv_W);
-        vp = div_rn_by(py + jy, P.fH, P.inv_H);
-      }
-      bdir = primary_dir(P, hp, vp);
-      bpos = cam;
-      br = bg = bb = 1.0f;
-      float t = -1.0f;
-      int ind = -1;
-      for (int w = 0; w < nwords; ++w) {
-        unsigned long long m = cmask[j * nwords + w];
-        m = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
-            (unsigned)__builtin_amdgcn_readfirstlane((unsigned)m);
-        while (m) {
-          const int i = (w << 6) + pop_lowest(m);
-          sphere_candidate(bpos, bdir, geo[i], i, 0.0001f, t, ind);
-        }
-      }
-      ++nseg;
-      if (ind != -1 && !(aux[ind].x > 0.9f)) {  // get_pt_within_unit_sphere(aa), hoisted (lazy)
-        float4 f = rbuf[2 * aa], sv = rbuf[2 * aa + 1];
-        float a = grandom(f.x + px * sv.z, f.y + py * sv.w);
-        float b = grandom(f.z - px * sv.z, f.w - py * sv.w);
-        float e = grandom(sv.x * px + sv.z, sv.y * py + sv.w);
-        bhemi = normalize(mk(a * 2.0f - 1.0f, b * 2.0f - 1.0f, e * 2.0f - 1.0f));
-      }
-      live = shade(ind, t, bpos, bdir, bhemi, br, bg, bb, D, bitem, true);
-    }
-    const unsigned long long fm = __ballot(bitem < bend && !live);  // ended at the primary hit
-    if (lane == 0 && fm) sdone[s] += __popcll(fm);
-    unsigned long long lm = __ballot(live);
-    if (live) perm[__builtin_amdgcn_mbcnt_hi((unsigned)(lm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)lm, 0u))] = lane;
-    nlive = __popcll(lm);
-    cursor = 0;
-    next = bend;
-    __syncthreads();
-  };
-
-  for (int guard = 0; guard < (1 << 24); ++guard) {  // (bound: a bug must not hang the GPU)
-    for (;;) {
-      unsigned long long need = __ballot(!has);
-      if (need == 0) break;
-      if (cursor >= nlive) {
-        // retire finished sub-pools in order, freeing their ring slots
-        while (jcomb <= jcull && __builtin_amdgcn_readfirstlane(sdone[jcomb % R]) == sub_count(jcomb)) {
-          combine(jcomb);
-          ++jcomb;
-        }
-        if (next >= totalw) break;
-        const int j = next / SUBN;
-        if (j >= jcomb + R) break;  // ring full: run the stragglers' bounce rounds first
-        if (j > jcull) {
-          jcull = j;
-          if (__builtin_amdgcn_readfirstlane(sncull[j]) < 0) {  // empty frustum: written up front
-            if (lane == 0) sdone[j % R] = sub_count(j);
-            next = (j + 1) * SUBN < totalw ? (j + 1) * SUBN : totalw;
-            continue;
-          }
-        }
-        prepare(j);
-        continue;
-      }
-      int r = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
-      int take = __popcll(need) < nlive - cursor ? __popcll(need) : nlive - cursor;
-      bool get = !has && r < take;
-      int src = get ? perm[cursor + r] : lane;
-      float sx = __shfl(bpos.x, src), sy = __shfl(bpos.y, src), sz = __shfl(bpos.z, src);
-      float dx = __shfl(bdir.x, src), dy = __shfl(bdir.y, src), dz = __shfl(bdir.z, src);
-      float hx = __shfl(bhemi.x, src), hy = __shfl(bhemi.y, src), hz = __shfl(bhemi.z, src);
-      float cr = __shfl(br, src), cg = __shfl(bg, src), cb = __shfl(bb, src);
-      int ci = __shfl(bitem, src);
-      if (get) {
-        pos = mk(sx, sy, sz);
-        dir = mk(dx, dy, dz);
-        hemi = mk(hx, hy, hz);
-        rr = cr; rg = cg; rb = cb;
-        item = ci;
-        depth = D - 1;
-        has = true;
-      }
-      cursor += take;
-    }
-    if (__ballot(has) == 0) {
-      if (next >= totalw) break;
-      continue;  // the ring was full and every path has ended: the retire step frees it
-    }
-    exec_tests += (unsigned long long)nobj;
-    const bool had = has;
-    const int myslot = div_tps(div_spp(item)) % R;
-    if (has) {
-      float t;
-      int ind = closest_hit_pf(geo, nobj, pos, dir, 0.0001f, t);
-      ++nseg;
-      has = shade(ind, t, pos, dir, hemi, rr, rg, rb, depth, item, false);
-      depth -= 1;
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {  // finished samples per ring slot, one LDS add per slot
-      const unsigned long long fm = __ballot(had && !has && myslot == r);
-      if (lane == 0 && fm) sdone[r] += __popcll(fm);
-    }
-  }
-  while (jcomb <= jcull) {  // drain: every remaining sub-pool is complete
-    combine(jcomb);
-    ++jcomb;
-  }
-
-  if (P.counters) {
-    unsigned sg = wave_sum(nseg);
-    if (lane == 0) {
-      unsigned long long* c = P.counters + (blockIdx.x & (kCounterSlots - 1));
-      const unsigned long long segs = (unsigned long long)sg + fast_samples;
-      atomicAdd(&c[0 * kCounterSlots], (unsigned long long)totalw);
-      atomicAdd(&c[1 * kCounterSlots], segs);
-      atomicAdd(&c[3 * kCounterSlots], segs * (unsigned long long)nobj);
-      atomicAdd(&c[4 * kCounterSlots], 64ull * exec_tests);
-    }
-  }
-}
-
-#endif  // RTRT_AB
+// (the streaming AO kernel of rounds 1-2, rejected in DESIGN.md §5, was removed in round 2)
 
 // ---------------------------------------------------------------------------------------
 // mode 1 pass 2 — aop_postprocessing.glsl:57-208, with the documented snapshot semantics:
@@ -2055,10 +1690,10 @@ void launch_batch(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStream_t str
 #if RTRT_AB
 // ---- A/B build only (make ablib -> build/librtrt_ab.so; tools/ab.py, tools/sections.py) -----
 // RTRT_AO_VARIANT selects an experimental AO kernel per launch: 9 (no first-bounce pre-test),
-// 27 (no batched first bounce), 17 (no split tail rounds), 11 (no lazy shortcuts), 20/25 (the
-// streaming sub-pool kernel, 7 / 6 waves), 91-93 (timing ablations: bounce tests twice, culled
-// primary tests twice, section clocks), 0/2 (the lane-per-sample kernel, LDS table / scalar
-// table).  RTRT_GENERAL=1 runs every program on the unculled LDS-table kernels (the pre-plane-
+// 27 (no batched first bounce), 17 (no split tail rounds), 11 (no lazy shortcuts), 91-93 (timing
+// ablations: bounce tests twice, culled primary tests twice, section clocks), 96/97 (section
+// clocks with the first bounce split, event counts), 0/2 (the lane-per-sample kernel, LDS table /
+// scalar table).  RTRT_GENERAL=1 runs every program on the unculled LDS-table kernels (the pre-plane-
 // support path for scenes with planes).  RTRT_B1_MIN: least live lanes for a batched first bounce.
 static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t stream, long long npix) {
   const char* ev = getenv("RTRT_AO_VARIANT");
@@ -2114,18 +1749,7 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true>), g, b, psh, stream, q, q.sph);
   else if (variant == 93)
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, false, true>), g, b, psh, stream, q, q.sph);
-  else if (variant == 20 || variant == 25) {
-    constexpr int kSub = 128, kRing = 2, kWaveSub = 8;  // sub-pool samples, ring slots, sub-pools per wave
-    const int TPs = kSub / p.spp > 0 ? kSub / p.spp : 1;
-    const long long waves = (npix + (long long)kWaveSub * TPs - 1) / ((long long)kWaveSub * TPs);
-    const size_t sh2 = stream_lds_bytes(p.spp, p.nobj, kSub, kRing, kWaveSub);
-    if (variant == 25)
-      hipLaunchKernelGGL((ao_stream_kernel<6, kSub, kRing>), dim3((unsigned)waves), b, sh2, stream, q, q.sph, kWaveSub,
-                         1.0f / (float)TPs);
-    else
-      hipLaunchKernelGGL((ao_stream_kernel<7, kSub, kRing>), dim3((unsigned)waves), b, sh2, stream, q, q.sph, kWaveSub,
-                         1.0f / (float)TPs);
-  } else  // 17: without the split tail rounds
+  else  // 17: without the split tail rounds
     hipLaunchKernelGGL(ao_batch_kernel<7>, g, b, psh, stream, q, q.sph);
   return true;
 }
