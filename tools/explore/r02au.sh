@@ -1,5 +1,5 @@
 # A/B repeat at config d (HEAD vs working tree), 2 x 6 rounds
-O=gpurun_out/r02as; mkdir -p $O
+O=gpurun_out/r02au; mkdir -p $O
 L=build/old/librtrt.so,real_time_ray_tracer_amd/librtrt.so
 for k in 1 2; do
   timeout -k 10 250 python tools/ab.py --config d --libs $L --rounds 5 --frames 5 > $O/d$k.txt 2>&1 || exit $?
