@@ -139,3 +139,29 @@ def test_c_driver_links_against_the_abi(gpu_available):
     p = subprocess.run([str(_headless()), "--width", "64", "--height", "48", "--frames", "2"],
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 1 and "no HIP device" in p.stderr, (p.returncode, p.stderr)
+
+
+def pool_of_block(b: int, n: int, Q: int) -> int:
+    """ao_batch_kernel's workgroup -> pool map (rt_kernels.hip, XCD-balanced pool order): row r's
+    Q pools rotated by r; a trailing partial group keeps its order."""
+    r = b // Q
+    if (r + 1) * Q > n:
+        return b
+    c = b - r * Q + r % Q
+    return r * Q + (c - Q if c >= Q else c)
+
+
+@pytest.mark.parametrize("n,Q", [(518400, 240), (64800, 240), (8, 8), (100, 8), (1200, 16), (33, 8), (4000, 120)])
+def test_pool_rotation_is_a_bijection(n, Q):
+    m = [pool_of_block(b, n, Q) for b in range(n)]
+    assert sorted(m) == list(range(n))
+
+
+def test_pool_rotation_spreads_columns_over_xcds():
+    """Blocks are dealt round-robin to 8 XCDs (b mod 8): with 240 pools per row, every XCD takes
+    every pool-column residue mod 8 once per 8 rows (in plain row order it would always take the
+    same residue)."""
+    Q = 240
+    for xcd in range(8):
+        res = {pool_of_block(b, 8 * Q, Q) % Q % 8 for b in range(8 * Q) if b % 8 == xcd}
+        assert res == set(range(8))
