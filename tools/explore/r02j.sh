@@ -1,4 +1,6 @@
-set -o pipefail
+# the driver's N=1 command on the final tree, twice
 O=gpurun_out/r02j; mkdir -p $O
-RTRT_LIB=build/librtrt_ab.so timeout -k 10 200 python tools/ab.py --config b --env RTRT_HY_ABL --variants 0,5,1,3 --rounds 5 --frames 40 --allow-diff > $O/ab_abl_b.txt 2>&1 || exit $?
-grep -o '"ms": {.*}}' $O/ab_abl_b.txt
+for k in 1 2; do
+  timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/b$k.json 2> $O/b$k.err || exit $?
+  python3 -c "import json;d=json.load(open('$O/b$k.json'));r=d['roofline'];print(d['value'],d['ms_per_step'],d['ms_per_step_median'],r['kernel_ms'],r['frac'],r['traffic_on_this_build'],(r.get('valu_issue') or {}).get('on_this_build'),d['cpu_baseline']['value'])"
+done
