@@ -566,7 +566,7 @@ def main():
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": desc, "width": W, "height": H, "spheres": S, "spp": spp, "mode": mode,
                        "max_depth": 20, "strips": plan.bounds,
-                       "parallelism": f"{world} row strip(s), cost-balanced" + (", RCCL gather to rank 0" if world > 1 else "")
+                       "parallelism": f"{world} row strip(s), cost-balanced" + ((", RCCL gather to rank 0" if args.backend == "nccl" else ", gloo gather to rank 0 (host-staged rehearsal)") if world > 1 else "")
                        + (", pipelined frames: consecutive AO passes on 2 alternating streams, post-process on a 3rd"
                           if pipeline else "")
                        + (", frame loop in C++ (rt_compute_frames)" if host_loop else "")

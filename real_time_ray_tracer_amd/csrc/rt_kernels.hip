@@ -163,11 +163,27 @@ struct FrameDst {
   float4* out_pix;
   float4* image;
 };
-__device__ __forceinline__ FrameDst frame_dst(const FrameParams& P) {
+__device__ __forceinline__ FrameDst frame_dst(const FrameParams& P, int j) {
   if (P.mf_n <= 0) return FrameDst{mk(P.Lx, P.Ly, P.Lz), P.out_pix, P.image};
-  const int j = blockIdx.z;
   const float4 L = P.mf_light[j];
   return FrameDst{mk(L.x, L.y, L.z), (float4*)P.hist_pix[(P.mf_slot0 + j) % P.F], j == P.mf_n - 1 ? P.image : nullptr};
+}
+// Multi-frame launches of modes 3/4 (FrameParams::mf_n frames): each block renders its tile in
+// frames blockIdx.z * FPB ... (up to FPB of them, one after another), so a launch dispatches FPB x
+// fewer workgroups and stages its LDS tables once per tile, not once per frame.  Every frame's
+// tile is traced and shaded in full.  Phong (config (a), short waves bound by the workgroup
+// dispatch rate): FPB 4, +5% over 1 (2: +3%, 8: +0%); hybrid (config (b)): 1 (2: -1.3%,
+// 4: -2.7%, 8: -17%; its waves are longer and the mirror bounces of a few tiles set the tail)
+// (tools/explore/r02m.sh).
+constexpr int kPhongFramesPerBlock = 4, kHybridFramesPerBlock = 1;
+template <int FPB>
+__device__ __forceinline__ int block_frames(const FrameParams& P, int& j0) {
+  if (P.mf_n <= 0) {
+    j0 = 0;
+    return 1;
+  }
+  j0 = (int)blockIdx.z * FPB;
+  return P.mf_n - j0 < FPB ? P.mf_n - j0 : FPB;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -572,7 +588,10 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
     else stage_shapes(P, lds);
     __syncthreads();
   }
-  phong_tile<ALLSPH, PL, LT>(P, lds, blockIdx.x, blockIdx.y, frame_dst(P));
+  int j0;
+  const int nj = block_frames<kPhongFramesPerBlock>(P, j0);
+#pragma unroll 1
+  for (int j = 0; j < nj; ++j) phong_tile<ALLSPH, PL, LT>(P, lds, blockIdx.x, blockIdx.y, frame_dst(P, j0 + j));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -777,8 +796,17 @@ __global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(FrameParams P) {
     else stage_shapes(P, lds);
     __syncthreads();
   }
-  hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x, blockIdx.y,
-                                             frame_dst(P));
+  if constexpr (kHybridFramesPerBlock == 1) {  // no frame loop (the loop form costs 3-4% at (b))
+    hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x, blockIdx.y,
+                                               frame_dst(P, blockIdx.z));
+  } else {
+    int j0;
+    const int nj = block_frames<kHybridFramesPerBlock>(P, j0);
+#pragma unroll 1
+    for (int j = 0; j < nj; ++j)
+      hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x, blockIdx.y,
+                                                 frame_dst(P, j0 + j));
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1797,7 +1825,9 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
     }
     return hipGetLastError();
   }
-  dim3 grid((p.W + 15) / 16, (p.trace_rows + 15) / 16, p.mf_n > 0 ? p.mf_n : 1);
+  // modes 3/4 multi-frame launches: FPB frames per block (block_frames)
+  const int fpb = program == K_PHONG ? kPhongFramesPerBlock : kHybridFramesPerBlock;
+  dim3 grid((p.W + 15) / 16, (p.trace_rows + 15) / 16, p.mf_n > 0 ? (p.mf_n + fpb - 1) / fpb : 1);
 #if RTRT_AB
   if (const char* ea = getenv("RTRT_HY_ABL"); ea && program == K_HYBRID && !pl && atoi(ea) > 0) {
     const int a = atoi(ea);

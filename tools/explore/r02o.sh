@@ -1,8 +1,8 @@
-# Phong 4 frames per block, hybrid 1: GPU suite, then configs a/b against the previous build (old)
+# Phong 4 frames per block, hybrid 1 without the frame loop: parity tests, then configs a/b against the previous build (old)
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r02n; mkdir -p $O
-timeout -k 10 700 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > $O/gpu_tests.txt 2>&1; rc=$?
+O=gpurun_out/r02o; mkdir -p $O
+timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/gpu_tests.txt 2>&1; rc=$?
 tail -2 $O/gpu_tests.txt; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   for v in old new; do
