@@ -78,6 +78,10 @@ def load():
     lib.rto_sphere_eval.restype = C.c_float
     lib.rto_normalize3.argtypes = [fp, fp]
     lib.rto_normalize3.restype = None
+    lib.rto_sphere_del.argtypes = [fp, fp, fp, C.c_float]
+    lib.rto_sphere_del.restype = C.c_float
+    lib.rto_primary_dir.argtypes = [fp, C.c_float, C.c_float, fp]
+    lib.rto_primary_dir.restype = None
     _lib = lib
     return lib
 
@@ -121,6 +125,27 @@ def random2(xy: np.ndarray) -> np.ndarray:
     f = load().rto_random
     xy = np.asarray(xy, np.float32).reshape(-1, 2)
     return np.array([f(float(a), float(b)) for a, b in xy], np.float32)
+
+
+def _f32v(v) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(v, np.float32).reshape(3))
+
+
+def sphere_del(pos, dir_, center, r) -> np.float32:
+    """The discriminant of sphere_eval_ray (p_compute.glsl:80-82) in the oracle's float semantics."""
+    return np.float32(load().rto_sphere_del(_fp(_f32v(pos)), _fp(_f32v(dir_)), _fp(_f32v(center)), float(r)))
+
+
+def sphere_eval(pos, dir_, center, r) -> np.float32:
+    return np.float32(load().rto_sphere_eval(_fp(_f32v(pos)), _fp(_f32v(dir_)), _fp(_f32v(center)), float(r)))
+
+
+def primary_dir(header: np.ndarray, hp, vp) -> np.ndarray:
+    """normalize(llc + hp*horizontal + vp*vertical) (p_compute.glsl:233-235) of a header."""
+    out = np.zeros(3, np.float32)
+    load().rto_primary_dir(_fp(np.ascontiguousarray(header, np.float32)), float(np.float32(hp)), float(np.float32(vp)),
+                           _fp(out))
+    return out
 
 
 def nthreads_default() -> int:

@@ -159,6 +159,13 @@ void rto_normalize3(const float v[3], float out[3]) {
   out[0] = n.x; out[1] = n.y; out[2] = n.z;
 }
 
+/* the discriminant of sphere_eval above (p_compute.glsl:80-82) */
+float rto_sphere_del(const float pos[3], const float dir[3], const float center[3], float r) {
+  v3 pmc = sub3(mk3(pos[0], pos[1], pos[2]), mk3(center[0], center[1], center[2]));
+  float b = dot3(mk3(dir[0], dir[1], dir[2]), pmc);
+  return fmaf(r, r, fmaf(b, b, -dot3(pmc, pmc)));
+}
+
 static float plane_eval(const octx* c, v3 pos, v3 dir, int i) {
   v3 n = mk3(SH(c, i, 0, 0), SH(c, i, 0, 1), SH(c, i, 0, 2));
   float denom = dot3(n, dir);
@@ -220,6 +227,15 @@ static int shadow_ray(const octx* c, v3 pos) {
 static v3 primary_dir(const octx* c, float hp, float vp) {
   v3 a = add3(c->llc, scl3(hp, c->horiz));
   return nrm3(add3(a, scl3(vp, c->vert)));
+}
+
+void rto_primary_dir(const float* h, float hp, float vp, float out[3]) {
+  octx c;
+  c.horiz = mk3(h[4 * RT_HDR_HORIZONTAL], h[4 * RT_HDR_HORIZONTAL + 1], h[4 * RT_HDR_HORIZONTAL + 2]);
+  c.vert = mk3(h[4 * RT_HDR_VERTICAL], h[4 * RT_HDR_VERTICAL + 1], h[4 * RT_HDR_VERTICAL + 2]);
+  c.llc = mk3(h[4 * RT_HDR_LLC_MINUS_CAMPOS], h[4 * RT_HDR_LLC_MINUS_CAMPOS + 1], h[4 * RT_HDR_LLC_MINUS_CAMPOS + 2]);
+  v3 d = primary_dir(&c, hp, vp);
+  out[0] = d.x; out[1] = d.y; out[2] = d.z;
 }
 
 static const float RT_GAMMA = 1.0f / 2.2f; /* p_compute.glsl:240 */

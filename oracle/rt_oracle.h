@@ -73,6 +73,11 @@ float rto_sin(float x);
 float rto_random(float x, float y);
 float rto_sphere_eval(const float pos[3], const float dir[3], const float center[3], float r);
 void rto_normalize3(const float v[3], float out[3]);
+/* the sphere discriminant fmaf(r, r, fmaf(b, b, -dot(pmc, pmc))) of sphere_eval_ray, and the
+ * primary direction normalize(llc + hp*horizontal + vp*vertical) of a header: used by the
+ * tests to construct exactly tangent rays (del == 0) */
+float rto_sphere_del(const float pos[3], const float dir[3], const float center[3], float r);
+void rto_primary_dir(const float* header, float hp, float vp, float out[3]);
 
 #ifdef __cplusplus
 }
