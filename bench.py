@@ -50,8 +50,12 @@ CONFIGS = {
                                  "AO 16 spp + post-process (mode 1)"),
     "s1": (3840, 2160, 10, 16, 1, "the reference's scene1 (4 spheres + 1 plane, src/scene.h:15-65) at 3840x2160, "
                                   "AO 16 spp + post-process (mode 1)"),
+    # the reference's own instance (src/main.cpp:29-36, 146, 309): 440x330, NUM_SHAPES 10, AA 4,
+    # scene1 (4 spheres + 1 plane), lighting 1 = aop_compute + aop_postprocessing
+    "ref": (440, 330, 10, 4, 1, "the reference's own instance: 440x330, NUM_SHAPES 10, AA 4, scene1 (4 spheres + 1 plane), "
+                                "lighting 1 = AO + post-process (src/main.cpp:29-36, 146, 309)"),
 }
-CONFIG_INDEX = {"a": 0, "b": 1, "c": 2, "d": 3, "e": 4, "p": 3, "q": 3, "s1": 3}
+CONFIG_INDEX = {"a": 0, "b": 1, "c": 2, "d": 3, "e": 4, "p": 3, "q": 3, "s1": 3, "ref": 3}
 
 
 def config_header(name: str):
@@ -60,7 +64,7 @@ def config_header(name: str):
     from real_time_ray_tracer_amd import Header, aspect_for
 
     W, H, S, spp, _, _ = CONFIGS[name]
-    if name == "s1":
+    if name in ("s1", "ref"):
         return Header.builtin(1, spp, aspect_for(W, H), num_shapes=S)
     if name in ("p", "q"):
         h = Header.synthetic(S - 1, spp, 1234 + CONFIG_INDEX[name], aspect_for(W, H), num_shapes=S)
@@ -146,6 +150,45 @@ def cpu_baseline(cfg_name: str, target_s: float) -> dict:
                       f"{t / (len(rows) * FR) * H * 1e3:.0f}"}
 
 
+def ssbo_path(cfg_name: str, gpu: int, frames: int = 30) -> dict:
+    """The reference's own call shape, timed: every frame copies the whole host SSBO in, runs the
+    program(s) and copies the whole SSBO (and the image) back (compute_one_shader /
+    compute_two_shaders, src/main.cpp:580-671), through rt_compute_one/two_shaders.  PCIe-inclusive;
+    never the headline value (that one keeps the inputs resident in HBM)."""
+    from real_time_ray_tracer_amd import (AO_COMPUTE, AOP_COMPUTE, AOP_POSTPROCESSING, H_COMPUTE, P_COMPUTE, SSBO,
+                                          Renderer)
+
+    W, H, S, spp, mode, _ = CONFIGS[cfg_name]
+    h = config_header(cfg_name)
+    s = SSBO(h, W, H)
+    img = np.zeros((H, W, 4), np.float32)
+    r = Renderer(W, H, S, spp, device=gpu)
+    f = 0
+
+    def one(k, f):
+        if mode in (1, 2):
+            h.fill_rand_buffer(7000 + k)
+        else:
+            h.moving_light(False)
+        s.set_header(h)
+        if mode == 1:
+            return r.compute_two_shaders(s, f, AOP_COMPUTE, AOP_POSTPROCESSING, img)
+        return r.compute_one_shader(s, f, {2: AO_COMPUTE, 3: P_COMPUTE, 4: H_COMPUTE}[mode], img)
+
+    for k in range(4):
+        f = one(k, f)
+    t0 = time.perf_counter()
+    for k in range(4, 4 + frames):
+        f = one(k, f)
+    dt = (time.perf_counter() - t0) / frames
+    r.close()
+    nbytes = s.data.nbytes
+    return {"ms_per_frame": round(dt * 1e3, 4), "mrays_per_s": round(W * H * (spp if mode in (1, 2) else 1) / dt / 1e6, 2),
+            "frames": frames, "ssbo_bytes": nbytes, "pcie_bytes_per_frame": 2 * nbytes + img.nbytes,
+            "call": "rt_compute_two_shaders (whole SSBO in and out, src/main.cpp:622-671)" if mode == 1
+            else "rt_compute_one_shader (whole SSBO in and out, src/main.cpp:580-620)"}
+
+
 VALU_FMA_RATE = 116.7e12 / 128  # wave64 v_fma_f32 instructions/s a dense stream sustains (profiles/r01g_valu_rate.txt)
 
 
@@ -205,7 +248,8 @@ def main():
                          "time has passed on every rank, so the timed frames run at settled GPU clocks: the "
                          "clock ramps over ~10 ms of load (DVFS), longer than 20 strip frames at N = 8")
     ap.add_argument("--verify", action="store_true",
-                    help="rank 0 also renders every frame whole and checks the gathered frames bit for bit")
+                    help="rank 0 also renders every frame whole and checks the gathered frames bit for bit "
+                         "(without it, N > 1 still checks the first 2 gathered frames, before the timed region)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N>1 path with ranks sharing GPUs, gather staged through host")
     args = ap.parse_args()
@@ -328,7 +372,11 @@ def main():
     gather = StripGather(plan, rank, dev, host_staging=args.backend == "gloo") if world > 1 else None
     state = {"frame": 0, "ref_frame": 0, "mismatch": 0, "checked": 0}
     ref = None
-    if args.verify and rank == 0:
+    # rank 0 checks gathered frames against a whole-frame render of its own: every frame with
+    # --verify, otherwise (N > 1) the first VERIFY_FIRST frames, during the warm-up, so every
+    # multi-GPU line carries correctness evidence without touching the timed region
+    VERIFY_FIRST = 2
+    if (args.verify or world > 1) and rank == 0:
         ref = Renderer(W, H, S, spp, device=gpu)
         ref.set_stream(stream)
 
@@ -367,7 +415,7 @@ def main():
         if gather is not None:
             with torch.cuda.stream(streams["out"]):
                 gather.gather(k)
-        if ref is not None:
+        if ref is not None and (args.verify or k < VERIFY_FIRST):
             verify(k)
 
     # One GPU, sequential modes: the frame loop runs in C++ (rt_compute_frames, the render loop of
@@ -583,9 +631,14 @@ def main():
             sm = strip_ms.cpu().tolist()
             balance_info.update({"strip_ms": [round(t, 4) for t in sm], "imbalance": round(imbalance(sm), 4)})
             out["config"]["balance"] = balance_info
-        if args.verify:
+        if ref is not None:
             out["verify"] = {"frames_checked": state["checked"], "mismatched": state["mismatch"],
+                             "what": ("every frame" if args.verify else f"the first {VERIFY_FIRST} frames (warm-up)")
+                             + ": the gathered frame vs a whole-frame render on rank 0, bit for bit",
                              "diag": state.get("diag", [])[:6]}
+        if world > 1:
+            out["collective"] = {"backend": args.backend if args.backend == "gloo" else "nccl (RCCL)",
+                                 "world_size": dist.get_world_size(), "op": "batch_isend_irecv strip gather to rank 0"}
         if mode == 1:
             # standalone launches: in the pipelined timed region the post-process shares the GPU
             # with the next frame's AO pass, so its event span is not a kernel duration
@@ -600,6 +653,8 @@ def main():
                                     "bytes_per_launch": round(post_bytes),
                                     "history_slots_read_per_pixel": round(counts["history_read"] / max(counts["post_pixels"], 1), 3),
                                     "traffic": traffic_data.get("2") if traffic_data else None}
+        if world == 1 and args.config in ("ref", "a"):
+            out["ssbo_path"] = ssbo_path(args.config, gpu)
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)

@@ -95,6 +95,13 @@ void* rt_get_stream(rt_ctx* ctx);
  * all streams before the main stream) see finished frames.  Off by default. */
 int rt_enable_pipelining(rt_ctx* ctx, int on, void* output_stream);
 void* rt_get_output_stream(rt_ctx* ctx);
+/* The stream of the last launch that wrote the context's image (the output stream for a
+ * pipelined mode-1 frame, the main stream for every other program); a consumer of the image
+ * (a copy, a collective) orders itself after it.  The next image writer is ordered after
+ * whatever was enqueued on that stream before it. */
+void* rt_image_stream(rt_ctx* ctx);
+/* Number of visible HIP devices (0 when none). */
+int rt_device_count(void);
 /* Wait for all of the context's work (both streams). */
 int rt_synchronize(rt_ctx* ctx);
 int rt_last_hip_error(rt_ctx* ctx);
@@ -155,12 +162,21 @@ int rt_compute_two_shaders(rt_ctx* ctx, void* ssbo, int frame_num, int program1,
  * (devices may repeat: several strips on one GPU), each an rt_ctx with its own g-buffer ring
  * (+ 1-row halo, so strips never exchange data), and assembles the image strips into one
  * [H][W] rgba32f frame on devices[0]: root-device strips render into their frame rows, the
- * others copy their strip over xGMI (peer access) on their output stream.  One host thread per
- * strip enqueues its work.  Results equal a whole-frame rt_ctx bit for bit. */
+ * others copy their strip over xGMI (peer access) on the stream that wrote their image
+ * (rt_image_stream).  One host thread per strip enqueues its work.  Results equal a
+ * whole-frame rt_ctx bit for bit. */
 typedef struct rt_group rt_group;
 /* cfg: the whole frame (row_begin/row_end ignored); bounds: n+1 increasing rows from 0 to H,
- * or NULL for equal strips. */
+ * or NULL for equal strips.  Fails with RT_E_NODEV for a device ordinal that does not exist and
+ * when peer access from a strip's device to devices[0] cannot be enabled (the strip copies
+ * would silently go through host memory). */
 int rt_group_create(int n, const int* devices, const rt_config* cfg, const int* bounds, rt_group** out);
+/* Strip i's copy path: 1 = its image is copied into the frame (another device, peer access
+ * on, or forced below), 0 = it renders straight into its frame rows; < 0 on a bad argument. */
+int rt_group_strip_copies(rt_group* g, int i);
+/* Test hook: on != 0 makes every strip but strip 0 render into its own image and copy it into
+ * the frame, even on the root device (the copy path of distinct devices, on one GPU). */
+int rt_group_force_copies(rt_group* g, int on);
 int rt_group_destroy(rt_group* g);
 int rt_group_size(rt_group* g);
 int rt_group_bounds(rt_group* g, int* bounds);          /* n+1 entries */

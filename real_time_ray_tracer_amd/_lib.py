@@ -47,6 +47,8 @@ SIGNATURES = {
     "rt_get_stream": (_vp, [_ctx]),
     "rt_enable_pipelining": (C.c_int, [_ctx, C.c_int, _vp]),
     "rt_get_output_stream": (_vp, [_ctx]),
+    "rt_image_stream": (_vp, [_ctx]),
+    "rt_device_count": (C.c_int, []),
     "rt_synchronize": (C.c_int, [_ctx]),
     "rt_last_hip_error": (C.c_int, [_ctx]),
     "rt_upload_header": (C.c_int, [_ctx, _vp, C.c_size_t]),
@@ -65,6 +67,8 @@ SIGNATURES = {
                                   C.POINTER(_grp)]),
     "rt_group_destroy": (C.c_int, [_grp]),
     "rt_group_size": (C.c_int, [_grp]),
+    "rt_group_strip_copies": (C.c_int, [_grp, C.c_int]),
+    "rt_group_force_copies": (C.c_int, [_grp, C.c_int]),
     "rt_group_bounds": (C.c_int, [_grp, C.POINTER(C.c_int)]),
     "rt_group_set_bounds": (C.c_int, [_grp, C.POINTER(C.c_int)]),
     "rt_group_strip": (_ctx, [_grp, C.c_int]),

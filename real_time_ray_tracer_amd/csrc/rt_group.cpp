@@ -7,9 +7,11 @@
 // into one [H][W] rgba32f frame on the root device (devices[0]):
 //   - a strip on the root device renders straight into its rows of the frame (rt_bind_image);
 //   - a strip on another device renders into its own image and copies it into the frame with
-//     one device-to-device copy over xGMI (peer access enabled), enqueued on the strip's output
-//     stream right behind the pass that writes it (the post-process when pipelined), so frame
-//     k's copy overlaps frame k+1's trace passes.
+//     one device-to-device copy over xGMI (peer access enabled), enqueued on the stream of the
+//     pass that wrote the image (rt_image_stream: the post-process's output stream for a
+//     pipelined mode-1 frame, the main stream otherwise), so frame k's copy follows that pass
+//     and overlaps frame k+1's trace passes; the next pass that writes the image is ordered
+//     after everything on that stream, the copy included.
 // Each strip keeps its own g-buffer ring for its rows plus a 1-row halo (rt_create), so no
 // strip reads another's data: the copies into the frame are the only transfers.
 // One host thread per strip enqueues its strip's work, so the per-frame host cost does not add
@@ -113,11 +115,13 @@ struct rt_group {
   bool have_header = false;
   Workers* workers = nullptr;
   int last_hip = 0;
+  bool force_copies = false;  // test hook: every strip but strip 0 takes the copy path
 };
 
 namespace {
 
-bool on_root(const rt_group* g, int i) { return g->devices[i] == g->devices[0]; }
+// strip i renders straight into its rows of the frame (no copy)
+bool on_root(const rt_group* g, int i) { return g->devices[i] == g->devices[0] && (i == 0 || !g->force_copies); }
 
 void destroy_strips(rt_group* g) {
   for (auto*& c : g->ctx)
@@ -155,8 +159,9 @@ int make_strips(rt_group* g) {
   return bind_strips(g);
 }
 
-// The image copy of strip i into its frame rows (strips off the root device), on the strip's
-// output stream behind the pass that wrote the image.
+// The image copy of strip i into its frame rows (strips off the root device), on the stream of
+// the pass that wrote the image (read after write), so the next writer of the image, ordered
+// after that stream's work, cannot overwrite it under the copy (write after read).
 int copy_strip(rt_group* g, int i) {
   if (on_root(g, i)) return RT_OK;
   const int W = g->cfg.width;
@@ -164,7 +169,7 @@ int copy_strip(rt_group* g, int i) {
   hipError_t e = hipSetDevice(g->devices[i]);
   if (e == hipSuccess)
     e = hipMemcpyAsync(g->frame + (size_t)g->bounds[i] * W, rt_image_device_ptr(g->ctx[i]), bytes,
-                       hipMemcpyDeviceToDevice, (hipStream_t)rt_get_output_stream(g->ctx[i]));
+                       hipMemcpyDeviceToDevice, (hipStream_t)rt_image_stream(g->ctx[i]));
   if (e != hipSuccess) {
     g->last_hip = (int)e;
     return RT_E_HIP;
@@ -265,14 +270,24 @@ int rt_group_create(int n, const int* devices, const rt_config* cfg, const int* 
   g->header.assign(rt_header_bytes(std::max(0, cfg->num_shapes), std::max(1, cfg->spp)) / 4, 0.0f);
   g->strip_header.assign(n, g->header);
   g->header_dirty.assign(n, 1);
-  // peer access root <-> every other device (the strip copies go over xGMI)
+  // peer access from every other device to the root (the strip copies go over xGMI).  Without
+  // it a device-to-device copy is staged through host memory: refuse instead of degrading
+  // silently.
   for (int i = 1; i < n; ++i) {
     const int d = g->devices[i], r = g->devices[0];
     if (d == r) continue;
     int can = 0;
-    if (hipDeviceCanAccessPeer(&can, d, r) == hipSuccess && can && hipSetDevice(d) == hipSuccess) {
-      hipError_t e = hipDeviceEnablePeerAccess(r, 0);
-      if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+    hipError_t e = hipDeviceCanAccessPeer(&can, d, r);
+    if (e == hipSuccess && !can) e = hipErrorPeerAccessUnsupported;
+    if (e == hipSuccess) e = hipSetDevice(d);
+    if (e == hipSuccess) {
+      e = hipDeviceEnablePeerAccess(r, 0);
+      if (e == hipErrorPeerAccessAlreadyEnabled) e = hipSuccess;
+    }
+    (void)hipGetLastError();  // no stale error for later launches to report
+    if (e != hipSuccess) {
+      delete g;
+      return RT_E_NODEV;
     }
   }
   hipError_t e = hipSetDevice(g->devices[0]);
@@ -314,6 +329,21 @@ int rt_group_destroy(rt_group* g) {
 }
 
 int rt_group_size(rt_group* g) { return g ? g->n : RT_E_INVAL; }
+
+int rt_group_strip_copies(rt_group* g, int i) {
+  if (!g || i < 0 || i >= g->n) return RT_E_INVAL;
+  return on_root(g, i) ? 0 : 1;
+}
+
+int rt_group_force_copies(rt_group* g, int on) {
+  if (!g) return RT_E_INVAL;
+  for (auto* c : g->ctx) {  // the frame rows may still be written
+    int rc = rt_synchronize(c);
+    if (rc != RT_OK) return rc;
+  }
+  g->force_copies = on != 0;
+  return bind_strips(g);
+}
 
 int rt_group_bounds(rt_group* g, int* bounds) {
   if (!g || !bounds) return RT_E_INVAL;

@@ -9,8 +9,10 @@
 //               [--scene synthetic|1|5|6] [--seed S] [--device D] [--ppm out.ppm] [--pipeline 0|1]
 //               [--strips G] [--devices d0,d1,...] [--balance ROUNDS]
 // --strips G > 1 renders the frame as G row strips through the rt_group_* entry points: strip i
-// on device devices[i % #devices] (default: every visible device in turn, or --device), cost-
-// balanced with --balance ROUNDS timed plans (0: equal strips), assembled on the first device.
+// on device devices[i % #devices] (default, without --devices: every visible device in turn,
+// starting at --device), cost-balanced with --balance ROUNDS timed plans (0: equal strips),
+// assembled on the first device.  A --devices list naming a device that does not exist, or
+// more devices than are visible, is refused with a message.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -55,18 +57,34 @@ static int run_strips(const rt_config& cfg, std::vector<float>& header, int mode
     devs.push_back(std::atoi(devlist.substr(p, q - p).c_str()));
     p = q + 1;
   }
-  if (devs.empty()) devs.push_back(device);
+  const int ndev = rt_device_count();
+  if (ndev <= 0) {
+    std::fprintf(stderr, "rt_headless: no HIP device is visible\n");
+    return 1;
+  }
+  if (devs.empty()) {
+    for (int k = 0; k < ndev; ++k) devs.push_back((device + k) % ndev);
+  } else {
+    // (every entry < ndev also bounds the distinct devices by the visible ones)
+    for (int d : devs)
+      if (d < 0 || d >= ndev) {
+        std::fprintf(stderr, "rt_headless: --devices names device %d, but only %d device(s) are visible (0..%d)\n",
+                     d, ndev, ndev - 1);
+        return 1;
+      }
+  }
   std::vector<int> sd(strips);
   for (int i = 0; i < strips; ++i) sd[i] = devs[i % devs.size()];
   rt_group* g = nullptr;
-  check(rt_group_create(strips, sd.data(), &cfg, nullptr, &g), "rt_group_create");
+  check(rt_group_create(strips, sd.data(), &cfg, nullptr, &g), "rt_group_create (peer access to the first device?)");
   if (pipeline) check(rt_group_enable_pipelining(g, 1), "rt_group_enable_pipelining");
   std::vector<double> strip_ms(strips, 0.0);
   if (balance > 0) check(rt_group_balance(g, header.data(), mode, balance, strip_ms.data()), "rt_group_balance");
   std::vector<int> b(strips + 1);
   check(rt_group_bounds(g, b.data()), "rt_group_bounds");
   std::printf("strips:");
-  for (int i = 0; i < strips; ++i) std::printf(" [%d,%d)@%d", b[i], b[i + 1], sd[i]);
+  for (int i = 0; i < strips; ++i)
+    std::printf(" [%d,%d)@%d%s", b[i], b[i + 1], sd[i], rt_group_strip_copies(g, i) > 0 ? "+copy" : "");
   std::printf("\n");
   auto t0 = std::chrono::steady_clock::now();
   check(rt_group_compute_frames(g, header.data(), mode, 0, frames, 7000, 0), "rt_group_compute_frames");

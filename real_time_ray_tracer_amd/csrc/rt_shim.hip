@@ -86,6 +86,7 @@ struct rt_ctx {
   bool out_pending = false;
   float4* d_image_own = nullptr;
   float4* d_image = nullptr;
+  hipStream_t img_stream = nullptr;  // the stream of the last launch that wrote the image
   std::vector<float> header;   // host copy of the SSBO prefix
   std::vector<float4> table;   // host copy of the device table (rt::table_vec4 float4)
   bool have_header = false;
@@ -302,6 +303,7 @@ int launch(rt_ctx* c, int program, const rt::FrameParams& p, hipStream_t st) {
   }
   hipError_t e = rt::launch_program(program, p, st);
   if (e != hipSuccess) return hip_fail(c, e);
+  if (p.image) c->img_stream = st;  // consumers of the image order their reads after this stream
   if (c->timing) {
     RT_HIP(c, hipEventRecord(e1, st));
     c->pending[program].push_back(rt_ctx::Timed{e0, e1, p.mf_n > 0 ? p.mf_n : 1});
@@ -609,6 +611,7 @@ int rt_set_stream(rt_ctx* c, void* s) {
   c->out_pending = false;
   for (auto& r : c->post_recorded) r = false;
   c->pipe_n = 0;
+  c->img_stream = nullptr;  // everything is finished (sync_all above)
   c->stream = (hipStream_t)s;  // NULL = the legacy NULL stream
   if (!c->pipelined) c->out_stream = c->stream;
   // an idle own stream is released: every stream holds one of the process's few hardware
@@ -635,6 +638,7 @@ int rt_enable_pipelining(rt_ctx* c, int on, void* output_stream) {
   c->out_pending = false;
   for (auto& r : c->post_recorded) r = false;
   c->pipe_n = 0;
+  c->img_stream = nullptr;
   c->pipelined = on != 0;
   if (!c->pipelined) {
     c->out_stream = c->stream;
@@ -655,6 +659,20 @@ int rt_enable_pipelining(rt_ctx* c, int on, void* output_stream) {
 void* rt_get_output_stream(rt_ctx* c) { return c ? (void*)c->out_stream : nullptr; }
 
 void* rt_get_stream(rt_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+void* rt_image_stream(rt_ctx* c) {
+  if (!c) return nullptr;
+  return (void*)(c->img_stream ? c->img_stream : c->stream);
+}
+
+int rt_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
 
 int rt_synchronize(rt_ctx* c) {
   if (!c) return RT_E_INVAL;

@@ -22,11 +22,21 @@ def equal_bounds(H: int, n: int) -> list[int]:
     return [round(i * H / n) for i in range(n + 1)]
 
 
-def balanced_bounds(row_cost: np.ndarray, n: int) -> list[int]:
+def balanced_bounds(row_cost: np.ndarray, n: int, min_rows: int | None = None) -> list[int]:
     """Contiguous strips of (nearly) equal total cost, row_cost[y] >= 0 for every frame row:
-    the C ABI's host-only planner (rt_plan_strips), shared with the one-process rt_group path."""
+    the C ABI's host-only planner (rt_plan_strips, no GPU call), shared with the one-process
+    rt_group path, so both drivers split frames identically.  It needs librtrt.so built (it
+    loads without a GPU).  min_rows is deprecated: every strip has at least one row, and a
+    larger minimum is no longer supported (it raises rather than being ignored)."""
     from .host import plan_strips
 
+    if min_rows is not None:
+        import warnings
+
+        warnings.warn("balanced_bounds(min_rows=...) is deprecated; strips have >= 1 row", DeprecationWarning,
+                      stacklevel=2)
+        if min_rows > 1:
+            raise ValueError("min_rows > 1 is no longer supported by rt_plan_strips")
     return plan_strips(row_cost, n)
 
 

@@ -385,6 +385,15 @@ class StripGroup:
         self._c(self._lib.rt_group_set_bounds(self.g, (C.c_int * (self.n + 1))(*[int(b) for b in bounds])),
                 "rt_group_set_bounds")
 
+    def strip_copies(self, i: int) -> bool:
+        """Whether strip i's image is copied into the frame (another device, or forced)."""
+        return bool(self._c(self._lib.rt_group_strip_copies(self.g, i), "rt_group_strip_copies"))
+
+    def force_copies(self, on: bool = True):
+        """Test hook: every strip but strip 0 renders into its own image and copies it into the
+        frame, as strips on other devices do (the copy path, exercised on one GPU)."""
+        self._c(self._lib.rt_group_force_copies(self.g, int(bool(on))), "rt_group_force_copies")
+
     def strip_ctx(self, i: int):
         return self._lib.rt_group_strip(self.g, i)
 

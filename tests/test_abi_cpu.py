@@ -141,6 +141,23 @@ def test_c_driver_links_against_the_abi(gpu_available):
     assert p.returncode == 1 and "no HIP device" in p.stderr, (p.returncode, p.stderr)
 
 
+def test_c_driver_strips_need_visible_devices(gpu_available):
+    """rt_headless --strips without a visible device stops with a message (rt_device_count), and
+    rt_group_create reports NODEV instead of building a group."""
+    import subprocess
+
+    if gpu_available:
+        pytest.skip("covered by the GPU run (test_gpu_group.py::test_headless_refuses_missing_devices)")
+    assert _lib.load().rt_device_count() == 0
+    p = subprocess.run([str(_headless()), "--width", "64", "--height", "48", "--strips", "2", "--devices", "0,1"],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 1 and "no HIP device is visible" in p.stderr, (p.returncode, p.stderr)
+    cfg = _lib.rt_config(64, 48, 10, 4, 8, 20, 0, 0)
+    g = C.c_void_p()
+    devs = (C.c_int * 2)(0, 1)
+    assert _lib.load().rt_group_create(2, devs, C.byref(cfg), None, C.byref(g)) == _lib.RT_E_NODEV
+
+
 def pool_of_block(b: int, n: int, Q: int) -> int:
     """ao_batch_kernel's workgroup -> pool map (rt_kernels.hip, XCD-balanced pool order): row r's
     Q pools rotated by r; a trailing partial group keeps its order."""

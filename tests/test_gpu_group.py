@@ -56,6 +56,50 @@ def test_group_frames_equal_whole_frame(mode, spp, frames, pipelined, G):
         assert_bitwise(g.image(), want, f"G={G} mode {mode}")
 
 
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_group_forced_copies_mixed_modes(pipelined):
+    """The copy path of strips on other devices (rt_group_force_copies: every strip but strip 0
+    renders into its own image and copies it into the frame), exercised on one GPU.  The copy
+    runs on the stream that wrote the strip's image: the output stream after a pipelined mode-1
+    frame, the main stream after modes 2-4 (which pipelined contexts still run on their main
+    stream), so frames switching modes must still assemble exactly."""
+    W, H, spp = 160, 120, 4
+    h = synth(W, H, 20, spp, seed=3)
+    modes = [1, 2, 1, 3, 4, 1, 1, 2, 4, 3, 1]
+    r = Renderer(W, H, h.S, h.AA)
+    if pipelined:
+        r.enable_pipelining(True)
+    with StripGroup(W, H, h.S, h.AA, devices(3)) as g:
+        if pipelined:
+            g.enable_pipelining(True)
+        g.force_copies(True)
+        assert [g.strip_copies(i) for i in range(3)] == [False, True, True]
+        hr, hg = h.copy(), h.copy()
+        fr = fg = 0
+        for k, mode in enumerate(modes):
+            for hh, f in ((hr, fr), (hg, fg)):
+                if mode in (1, 2):
+                    hh.fill_rand_buffer(7000 + k)
+                else:
+                    hh.moving_light(True)
+                hh.set_mode(f, hh.num_objects)
+            r.upload_header(hr)
+            fr = r.dispatch(mode, fr)
+            g.upload_header(hg)
+            fg = g.dispatch(mode, fg)
+            assert fr == fg
+            assert_bitwise(g.image(), r.image(), f"frame {k} (mode {mode})")
+        # and a burst of frames without a host round trip in between (the copies stay in flight)
+        for mode, n in ((1, 9), (2, 3), (4, 3)):
+            fr = r.compute_frames(hr, mode, fr, n, 9000, True)
+            fg = g.compute_frames(hg, mode, fg, n, 9000, True)
+            assert fr == fg
+            assert_bitwise(g.image(), r.image(), f"burst of {n} mode-{mode} frames")
+        g.force_copies(False)
+        assert not g.strip_copies(1)
+    r.close()
+
+
 def test_group_dispatch_per_frame_and_uneven_bounds():
     """The per-frame calls (upload_header + dispatch), uneven strips including a 1-row strip,
     and a scene with a plane (the reference's scene1)."""
@@ -134,6 +178,18 @@ def test_group_errors():
             g.dispatch(7, 0)
         with pytest.raises(RtError):
             g.set_bounds([0, 48, 48])
+
+
+def test_headless_refuses_missing_devices():
+    """rt_headless --devices naming a device that is not visible stops with a message."""
+    exe = ROOT / "build" / "rt_headless"
+    import torch
+
+    n = torch.cuda.device_count()
+    p = subprocess.run([str(exe), "--width", "64", "--height", "48", "--strips", "2", "--devices", f"0,{n}"],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 1
+    assert f"names device {n}" in p.stderr
 
 
 def test_headless_strips_ppm_equals_whole_frame(tmp_path):
