@@ -1,8 +1,9 @@
 # Build the MI355X library (HIP, gfx950) and the CPU oracle (test infrastructure).
 #   make            -> real_time_ray_tracer_amd/librtrt.so, oracle/build/librt_oracle.so, build/rt_headless
 #   make lib|oracle|headless|clean
-#   make ablib      -> build/librtrt_ab.so: the same library plus the experimental A/B kernels and
-#                      their RTRT_* environment switches (tools/ab.py: RTRT_LIB=build/librtrt_ab.so)
+#   make ablib      -> build/librtrt_ab.so: the same shim over tools/ab/rt_kernels_ab.hip, the launcher
+#                      with the experimental A/B kernels and their RTRT_* environment switches
+#                      (tools/ab.py: RTRT_LIB=build/librtrt_ab.so); never part of librtrt.so
 HIPCC    ?= /opt/rocm/bin/hipcc
 CC       ?= gcc
 ARCH     ?= gfx950
@@ -45,10 +46,10 @@ $(LIB): $(OBJDIR)/rt_kernels.o $(OBJDIR)/rt_shim.o $(OBJDIR)/rt_host.o $(OBJDIR)
 	 printf '{"src_sha1": "%s", "commit": "%s"}\n' "$$src" "$$commit" > $(PKG)/BUILD_INFO
 
 ABLIB := build/librtrt_ab.so
-$(OBJDIR)/ab_%.o: $(CSRC)/%.hip $(CSRC)/*.h include/rt/*.h | $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -DRTRT_AB=1 -x hip -c $< -o $@
+$(OBJDIR)/rt_kernels_ab.o: tools/ab/rt_kernels_ab.hip $(CSRC)/*.h include/rt/*.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -I$(CSRC) -x hip -c $< -o $@
 
-$(ABLIB): $(OBJDIR)/ab_rt_kernels.o $(OBJDIR)/ab_rt_shim.o $(OBJDIR)/rt_host.o $(OBJDIR)/rt_group.o
+$(ABLIB): $(OBJDIR)/rt_kernels_ab.o $(OBJDIR)/rt_shim.o $(OBJDIR)/rt_host.o $(OBJDIR)/rt_group.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 ablib: $(ABLIB)

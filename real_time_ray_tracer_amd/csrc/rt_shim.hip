@@ -526,10 +526,6 @@ int rt_create(int device, const rt_config* cfg, rt_ctx** out) {
   if (!x) return RT_E_NOMEM;
   x->device = device;
   x->cfg = c;
-#if RTRT_AB  // pipelining shape (A/B builds only): RTRT_PIPE_DEPTH in [2, kPipe], RTRT_AO_STREAMS in [1, kAoStreams]
-  if (const char* ev = getenv("RTRT_PIPE_DEPTH")) x->pipe_depth = std::min(kPipe, std::max(2, atoi(ev)));
-  if (const char* ev = getenv("RTRT_AO_STREAMS")) x->n_ao_streams = std::min(kAoStreams, std::max(1, atoi(ev)));
-#endif
   x->own0 = c.row_begin;
   x->own_rows = c.row_end - c.row_begin;
   x->band0 = std::max(0, c.row_begin - 1);

@@ -17,8 +17,10 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 SRC = ROOT / "real_time_ray_tracer_amd/csrc/rt_kernels.hip"
+AB_SRC = ROOT / "tools/ab/rt_kernels_ab.hip"  # the A/B tools library's launcher (make ablib)
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-ffp-contract=off",
-         "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize", f"-I{ROOT / 'include'}"]
+         "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize", f"-I{ROOT / 'include'}",
+         f"-I{ROOT / 'real_time_ray_tracer_amd/csrc'}"]
 FIELDS = ("VGPRs", "AGPRs", "TotalSGPRs", "ScratchSize [bytes/lane]", "Occupancy [waves/SIMD]", "SGPRs Spill",
           "VGPRs Spill", "LDS Size [bytes/block]")
 
@@ -31,7 +33,7 @@ def demangle(names):
 
 def main():
     ab = "--ab" in sys.argv
-    cmd = ["/opt/rocm/bin/hipcc", *FLAGS, *(["-DRTRT_AB=1"] if ab else []), "-x", "hip", "-c", str(SRC),
+    cmd = ["/opt/rocm/bin/hipcc", *FLAGS, "-x", "hip", "-c", str(AB_SRC if ab else SRC),
            "-o", "/dev/null", "--offload-device-only", "-Rpass-analysis=kernel-resource-usage"]
     text = subprocess.run(cmd, capture_output=True, text=True).stderr
     rows, cur = [], None
