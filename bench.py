@@ -81,11 +81,14 @@ PEAK_FP32_TFLOPS = 157.3    # MI355X_MICROARCH.md: peak FP32 vector (spec)
 PEAK_HBM_GBPS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 # algorithmic HBM bytes per pixel per launch: mode-1 pass 1 writes raw colour +
 # normal + depth (48 B); mode 2 also the image (64 B); modes 3/4 pixel + image (32 B).  The
-# post-process (pass 2) reads colour + normal + depth of its pixel (48 B; the 4 neighbours are
-# other pixels' bytes), 32 B (normal + depth) per history slot it examines and 16 B per slot
-# it accepts, and writes pixel + image (32 B): counted per launch from the kernel's counters.
+# post-process (pass 2, aop_postprocessing.glsl:57-208) needs, at minimum: per pixel its raw
+# colour (16 B) and its normal's hit flag w (4 B), and writes pixel + image (32 B); per filtered
+# pixel (a primary hit) also its normal xyz (12 B) and depth.xy (8 B: .z/.w are never read);
+# per history slot it examines the slot's normal xyz + depth.xy (20 B), and per slot it accepts
+# the slot's colour (16 B).  The 4 neighbours are other pixels' bytes.  Counted per launch from
+# the kernel's counters ([5] filtered pixels, [6] slots read, [7] slots accepted).
 BYTES_PER_PIXEL = {1: 48, 3: 64, 4: 32, 5: 32}
-POST_BYTES_PIXEL, POST_BYTES_SLOT_READ, POST_BYTES_SLOT_ACCEPTED = 80, 32, 16
+POST_BYTES_PIXEL, POST_BYTES_FILTERED, POST_BYTES_SLOT_READ, POST_BYTES_SLOT_ACCEPTED = 52, 20, 20, 16
 
 
 def log(*a):
@@ -644,15 +647,21 @@ def main():
             # with the next frame's AO pass, so its event span is not a kernel duration
             n_p, tot_p = solo[2]
             pms = tot_p / max(n_p, 1)
-            post_bytes = (POST_BYTES_PIXEL * counts["post_pixels"] + POST_BYTES_SLOT_READ * counts["history_read"]
+            post_px = (r1 - r0) * W * ncount  # every pixel of the strip, per counted launch
+            post_bytes = (POST_BYTES_PIXEL * post_px + POST_BYTES_FILTERED * counts["filtered_pixels"]
+                          + POST_BYTES_SLOT_READ * counts["history_read"]
                           + POST_BYTES_SLOT_ACCEPTED * counts["history_accepted"]) / ncount
             pbw = post_bytes / (pms * 1e-3) / 1e9
             out["roofline_post"] = {"bound": "hbm", "achieved": round(pbw, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                                     "frac": round(pbw / PEAK_HBM_GBPS, 4), "kernel": "aop_postprocessing (post_kernel)",
                                     "kernel_ms": round(pms, 4), "measured": "standalone (2 frames after the timed region)",
                                     "bytes_per_launch": round(post_bytes),
-                                    "history_slots_read_per_pixel": round(counts["history_read"] / max(counts["post_pixels"], 1), 3),
-                                    "traffic": traffic_data.get("2") if traffic_data else None}
+                                    "byte_model": "52 B/pixel + 20 B/filtered pixel + 20 B/history slot read + 16 B/slot accepted",
+                                    "filtered_fraction": round(counts["filtered_pixels"] / max(post_px, 1), 4),
+                                    "history_slots_read_per_filtered_pixel": round(counts["history_read"] / max(counts["filtered_pixels"], 1), 3),
+                                    "traffic": traffic_data.get("2") if traffic_data else None,
+                                    "traffic_over_model": (round(traffic_data["2"] / post_bytes, 3)
+                                                           if traffic_data and traffic_data.get("2") else None)}
         if world == 1 and args.config in ("ref", "a"):
             out["ssbo_path"] = ssbo_path(args.config, gpu)
         if world == 1 and not args.no_cpu_baseline:

@@ -230,7 +230,8 @@ int rt_host_stats(rt_ctx* ctx, double* wait_ms, long long* waits);
  * int(mode.z) — the algorithmic-FLOP basis of the roofline (20 FLOP per ray-sphere test,
  * SURVEY.md §8d), [4] executed lane-tests = sum over wavefronts of 64 x the shapes their scene
  * loops tested (divergence and culling: [3]/[4] is the useful fraction); post-process:
- * [5] filtered pixels, [6] history slots read, [7] history slots accepted. */
+ * [5] filtered pixels (those with a primary hit, normals.w > 0.99; the others are copied),
+ * [6] history slots read, [7] history slots accepted. */
 int rt_enable_counters(rt_ctx* ctx, int on);
 /* Read the 8 totals (synchronises); reset != 0 zeroes them afterwards. */
 int rt_read_counters(rt_ctx* ctx, uint64_t out[8], int reset);

@@ -21,6 +21,7 @@ struct FrameParams {
   int spp, D, F, frame;
   int b1_min;                // AO: least live lanes of a prepared batch for its batched first bounce (set at launch)
   int pool_rot;              // AO: pools per rotation group (one row's; 0 = pools in row order; set at launch)
+  int tile_run;              // post-process: tiles per XCD run (xcd_tile; set at launch)
   float inv_spp, fW, fH;     // 1.0f / spp, (float)W, (float)H: host-computed wave-uniform constants
   float inv_W, inv_H;        // 1.0f / fW, 1.0f / fH (correctly rounded; div_rn_by)
   float hx, hy, hz;          // horizontal
@@ -34,6 +35,10 @@ struct FrameParams {
   const float4* sph;         // [S] sphere-only geometry: geo for spheres, NaN for every other shape
   const float4* planes;      // [nplanes][2]: (normal, bits(index)), (p0, 0) of the planes among [0, nobj)
   int nplanes;               // set by the host (rt_shim) from the header's shape ids
+  // AO bounce-ray cluster culling (set by the host, rt_shim build_clusters; ncl = 0: off):
+  const float4* clus;        // [ncl] (centre, R): every member sphere lies within R of the centre
+  const unsigned long long* clmask;  // [1 + kMaxClusters][kClusterWords]: always-tested spheres, then members
+  int ncl;
   const float4* rb;          // rand_buffer[2*spp]
   float4* out_pix;           // colour destination [band_rows][W]
   float4* nrm;               // normals_buffer slot `frame` [band_rows][W]
@@ -63,15 +68,26 @@ struct FrameParams {
   const float4* mf_rb;
 };
 
+// Bounce-ray cluster culling (AO later bounce rounds): at most kMaxClusters clusters (a wave-uniform
+// u64 of kept clusters), member masks over the first kClusterWords * 64 spheres.
+constexpr int kMaxClusters = 64;
+constexpr int kClusterWords = 4;
+
 // Device shape table of one header copy, in float4 units from its base (rt_shim fills it):
 //   [0, 4S)          geo, geo2, col, aux        (rt_device.h "scene tables")
 //   [4S, 5S)         sph: geo of spheres, NaN of other shapes (never accepted by sphere_candidate)
 //   [5S, 7S)         planes: 2 float4 per plane, compacted, ascending index
-//   [7S, 7S + 2spp)  rand_buffer
+//   [7S, 7S + 64)    clusters: (centre, R) per cluster
+//   then (1 + 64) * 4 u64 cluster masks (the always-tested spheres, then each cluster's members)
+//   then rand_buffer[2 spp]
 __host__ __device__ constexpr size_t sphere_table(int S) { return (size_t)4 * S; }
 __host__ __device__ constexpr size_t plane_table(int S) { return (size_t)5 * S; }
-__host__ __device__ constexpr size_t rand_table(int S) { return (size_t)7 * S; }
-__host__ __device__ constexpr size_t table_vec4(int S, int spp) { return (size_t)7 * S + (size_t)2 * spp; }
+__host__ __device__ constexpr size_t cluster_table(int S) { return (size_t)7 * S; }
+__host__ __device__ constexpr size_t cluster_mask_table(int S) { return cluster_table(S) + kMaxClusters; }
+__host__ __device__ constexpr size_t rand_table(int S) {
+  return cluster_mask_table(S) + (size_t)(1 + kMaxClusters) * kClusterWords / 2;
+}
+__host__ __device__ constexpr size_t table_vec4(int S, int spp) { return rand_table(S) + (size_t)2 * spp; }
 
 enum KernelId { K_AOP = 1, K_POST = 2, K_AO = 3, K_PHONG = 4, K_HYBRID = 5 };
 

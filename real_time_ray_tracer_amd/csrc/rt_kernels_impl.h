@@ -157,6 +157,29 @@ __device__ __forceinline__ float4 dep_load(const float4* base, size_t n, size_t 
   return make_float4(a.x, a.y, b.x, b.y);
 }
 __device__ __forceinline__ float2 dep_load_xy(const float4* base, size_t off) { return ((const float2*)base)[off]; }
+// Normals g-buffer slot layout: a [band_rows][W] plane of xyz (12 B per pixel) then a
+// [band_rows][W] plane of w (the hit flag, 4 B).  The post-process's temporal test reads only
+// the history normals' xyz (aop_postprocessing.glsl:180), 12 B per history slot instead of 16;
+// the pixel itself and its neighbours read both planes.  rt_download / rt_upload_gbuffer convert
+// to the reference's vec4 layout.
+__device__ __forceinline__ void nrm_store(float4* base, size_t n, size_t off, float4 v) {
+  float* p = (float*)base;
+  p[3 * off] = v.x;
+  p[3 * off + 1] = v.y;
+  p[3 * off + 2] = v.z;
+  p[3 * n + off] = v.w;
+}
+__device__ __forceinline__ f3 nrm_load_xyz(const float4* base, size_t off) {
+  const float* p = (const float*)base;
+  return mk(p[3 * off], p[3 * off + 1], p[3 * off + 2]);
+}
+__device__ __forceinline__ float nrm_load_w(const float4* base, size_t n, size_t off) {
+  return ((const float*)base)[3 * n + off];
+}
+__device__ __forceinline__ float4 nrm_load(const float4* base, size_t n, size_t off) {
+  const f3 v = nrm_load_xyz(base, off);
+  return make_float4(v.x, v.y, v.z, nrm_load_w(base, n, off));
+}
 
 struct FrameDst {
   f3 light;
@@ -332,6 +355,39 @@ __device__ __forceinline__ bool bounce_cone_keep_pt(const ConeB& c, float4 g, fl
   const float K = c.ct * ca - c.st * sa - 2e-5f;
   const float cphi = c.ax * ux + c.ay * uy + c.az * uz;
   return !(cphi < K);  // (2)
+}
+
+// Bounce-ray cluster cull (ao_batch_kernel's later bounce rounds).  A cluster cb = (centre, R)
+// holds spheres with |c_i - centre| + |r_i| <= R (rt_shim build_clusters).  The ray (p, d), |d|
+// = 1 within 3e-7, provably accepts none of them when
+//  (A) its line passes the centre at distance h > R' = R + 0.0032 (Lmax + R), Lmax = |p - centre|
+//      + R >= |p - c_i|: then every member's line distance is h_i > r_i + sqrt(1e-5 (d_i^2 +
+//      r_i^2)) >= r_eff (the cone culls' inflated radius, d_i = |p - c_i|), so the exact
+//      discriminant is <= -1e-5 (d_i^2 + r_i^2), > 5x the computed one's float error:
+//      the computed del is < 0 (-1 in the reference, never accepted).  The computed h^2 =
+//      fmaf(-b, b, L2) is within ~1.3e-6 L2 of the exact one, covered by the 4e-6 L2 slack;
+//  (B) or the ball lies behind the origin (d . (centre - p) < -R' - 1e-3 (u + R')) while the
+//      origin is outside it (u - R' > 1e-2 (u + R'), u = |p - centre|): for every member the
+//      closest approach is behind (b_i > 0 with margin) and the origin is outside it by more than
+//      1e-2 (|p - c_i| + r_i), so both roots are negative by more than 10x the computed-root error
+//      (bounce_cone_misses (1)): never above the 1e-4 threshold.
+// NaN anywhere fails both tests and keeps the cluster.
+#ifndef RT_GLOBAL_TAIL
+#define RT_GLOBAL_TAIL 1  // config (e), 256 spheres: 140.6 -> 128.3 ms per frame (r03i)
+#endif
+#ifndef RT_CLUSTER_TAIL_MAX_G
+#define RT_CLUSTER_TAIL_MAX_G 8
+#endif
+constexpr int kClusterTailMaxG = RT_CLUSTER_TAIL_MAX_G;  // split tail rounds with G <= this use the cluster cull
+__device__ __forceinline__ bool cluster_may_hit(f3 p, f3 d, float4 cb) {
+  const float vx = cb.x - p.x, vy = cb.y - p.y, vz = cb.z - p.z;
+  const float L2 = fmaf(vz, vz, fmaf(vy, vy, vx * vx));
+  const float b = fmaf(d.z, vz, fmaf(d.y, vy, d.x * vx));  // > 0: the centre lies ahead
+  const float u = fast_sqrt(L2);
+  const float Rp = fmaf(0.0032f, u + 2.0f * cb.w, cb.w);
+  const bool line_miss = fmaf(-b, b, L2) > fmaf(Rp, Rp, 4e-6f * L2);
+  const bool behind = (b + Rp) < -1e-3f * (u + Rp) && (u - Rp) > 1e-2f * (u + Rp);
+  return !(line_miss || behind);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -882,12 +938,16 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   for (int k = lane; k < TP; k += 64) pstop[k] = -1;
   // TAIL: the sphere table in LDS (per-lane sphere indices in the split tail rounds)
   float4* geol = (float4*)(lbase + LO.geol);  // [nobj] when TAIL && nobj <= kTailMaxObj
-  const bool tail_ok = TAIL && nobj <= kTailMaxObj;
+  // split tail rounds: the sphere table in LDS up to kTailMaxObj spheres; above (TAIL instantiations
+  // launched without the LDS table), per-lane reads of the global table (L1/L2-resident)
+  const bool tail_lds = TAIL && nobj <= kTailMaxObj;
+  const bool tail_ok = TAIL;
+  const float4* const tgeo = tail_lds ? geol : geo;
   // PT: the batched first bounce keeps its per-ray pre-test table in the same LDS rows, so the
   // sphere table is (re)staged only when a split tail round needs it
-  const bool pt_ok = PT && B1 && tail_ok;
+  const bool pt_ok = PT && B1 && tail_lds;
   bool geol_valid = false;  // wave-uniform
-  if (tail_ok && !pt_ok) {
+  if (tail_lds && !pt_ok) {
     for (int k = lane; k < nobj; k += 64) geol[k] = geo[k];
     geol_valid = true;
   }
@@ -918,7 +978,9 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   unsigned long long tsec[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // 5..7: bounce rounds, sum ncull, prepares
   // ABL == 6: the same, with slots 5..7 timing the batched first bounce's cone + cull, survivor
   // loop and shading; ABL == 7: event counts of the first bounce and the bounce rounds instead
-  constexpr bool kLaps = ABL == 3 || ABL == 6;
+  // ABL == 8: the ABL == 3 sections with the later bounce rounds split: split tail rounds in slot
+  // 5, full rounds in slot 3; slots 6 / 7 count full / tail rounds
+  constexpr bool kLaps = ABL == 3 || ABL == 6 || ABL == 8;
   unsigned long long tmark = kLaps ? __builtin_amdgcn_s_memtime() : 0;
   auto lap = [&](int k) {
     if (kLaps) {
@@ -977,7 +1039,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       int x, y;
       pool_xy(lp, x, y);
       const size_t off = (size_t)(y - P.band_row0) * W + x;
-      f_nrm[off] = z;
+      nrm_store(f_nrm, dep_plane(P), off, z);
       dep_store(f_dep, dep_plane(P), off, z);  // (0, 0, 0, 0) / AA
       store_color(P, f_out, f_img, x, y, col);
       if (rowc) atomicAdd(&rowc[y - P.band_row0], (unsigned long long)spp);  // ~free
@@ -1269,7 +1331,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     // lowest index on ties = exactly the sequential scan's result (ao_compute.glsl:183-194).
     const int L = __popcll(hm);
     if (tail_ok && next >= total && cursor >= nlive && L <= 32) {
-      if (!geol_valid) {
+      if (tail_lds && !geol_valid) {
         __syncthreads();
         for (int k = lane_id_here(); k < nobj; k += 64) geol[k] = geo[k];
         geol_valid = true;
@@ -1287,8 +1349,42 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       const f3 d = mk(__shfl(dir.x, owner), __shfl(dir.y, owner), __shfl(dir.z, owner));
       float t = -1.0f;
       int ind = -1;
-      if (act)
-        for (int i = pl; i < nobj; i += G) sphere_candidate(o, d, geol[i], i, 0.0001f, t, ind);
+      if (P.ncl > 0 && G <= kClusterTailMaxG) {
+        // cluster cull over the round's L paths (cluster_may_hit): lane pl of group g tests
+        // clusters pl, pl + G, ... for path g; the ballot folded over the groups gives the clusters
+        // some path may hit.  Their spheres plus the always-tested ones, compacted in ascending
+        // order into a byte list (LDS: the primary cull mask's words, dead once the pool's samples
+        // are all prepared), are split over the group's lanes as before: the group merge below
+        // returns the lexicographic minimum (t, index) over them = the full scan's result.
+        unsigned long long kc = 0;
+        for (int c0 = 0; c0 < P.ncl; c0 += G) {
+          const int c = c0 + pl;
+          const bool may = act && c < P.ncl && cluster_may_hit(o, d, P.clus[c]);
+          unsigned long long b = __builtin_amdgcn_ballot_w64(may);
+          for (int sh = 32; sh >= G; sh >>= 1) b |= b >> sh;
+          kc |= (G == 64 ? b : (b & ((1ull << G) - 1))) << c0;
+        }
+        unsigned char* list = (unsigned char*)cmask;
+        int cnt = 0;
+        for (int w = 0; w < nwords; ++w) {
+          unsigned long long m = P.clmask[w];
+          for (unsigned long long k2 = kc; k2;) m |= P.clmask[(size_t)(1 + pop_lowest(k2)) * kClusterWords + w];
+          const int ln = lane_id_here();
+          if ((m >> ln) & 1ull)
+            list[cnt + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+                (unsigned char)((w << 6) + ln);
+          cnt += __popcll(m);
+        }
+        __syncthreads();  // the list is written (one wave per workgroup)
+        exec_tests += (unsigned long long)((P.ncl + G - 1) / G + (cnt + G - 1) / G);
+        if (act)
+          for (int k = pl; k < cnt; k += G) {
+            const int i = list[k];
+            sphere_candidate(o, d, tgeo[i], i, 0.0001f, t, ind);
+          }
+      } else if (act) {
+        for (int i = pl; i < nobj; i += G) sphere_candidate(o, d, tgeo[i], i, 0.0001f, t, ind);
+      }
       for (int m = 1; m < G; m <<= 1) {
         const float tb = __shfl_xor(t, m);
         const int ib = __shfl_xor(ind, m);
@@ -1298,18 +1394,19 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       }
       float tt = __shfl(t, rk * G);
       int ii = __shfl(ind, rk * G);
-      exec_tests += (unsigned long long)((nobj + G - 1) / G);
+      if (!(P.ncl > 0 && G <= kClusterTailMaxG)) exec_tests += (unsigned long long)((nobj + G - 1) / G);
       if (has) {
         if (PL) plane_pass(P, pos, dir, 0.0001f, tt, ii);
         ++nseg;
         has = shade(ii, tt, pos, dir, hemi, rr, rg, rb, depth, item, false);
         depth -= 1;
       }
-      lap(3);
+      if (ABL == 8) tsec[7] += 1;
+      lap(ABL == 8 ? 5 : 3);
       continue;
     }
     // ---- one bounce segment for every live path, against every sphere ------------------
-    exec_tests += (unsigned long long)nobj;
+    exec_tests += (unsigned long long)(P.ncl > 0 ? P.ncl : nobj);
     if (ABL == 7) {  // later bounce rounds: sphere iterations, and those with any live lane's del >= 0
       tsec[6] += (unsigned long long)nobj;
       for (int i = 0; i < nobj; ++i) {
@@ -1320,7 +1417,37 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         tsec[7] += __ballot(has && del >= 0.0f) != 0;
       }
     }
-    if (has) {
+    if (P.ncl > 0) {
+      // cluster cull: a cluster is skipped when no live lane's ray may hit it (cluster_may_hit);
+      // the spheres of the kept clusters plus the always-tested ones are visited in ascending
+      // index order, so (t, ind) is the full scan's (ao_compute.glsl:183-194)
+      unsigned long long kc = 0;
+      for (int c = 0; c < P.ncl; ++c) {
+        const bool may = has && cluster_may_hit(pos, dir, P.clus[c]);
+        if (__builtin_amdgcn_ballot_w64(may) != 0) kc |= 1ull << c;
+      }
+      float t = -1.0f;
+      int ind = -1;
+      for (int w = 0; w < nwords; ++w) {
+        unsigned long long m = P.clmask[w];
+        for (unsigned long long k2 = kc; k2;) m |= P.clmask[(size_t)(1 + pop_lowest(k2)) * kClusterWords + w];
+        exec_tests += (unsigned long long)__popcll(m);
+        if (has) {
+          // (streaming the word's 4-sphere groups with a per-nibble skip, or loading 4 survivors
+          // per wait, were slower: configs d / e +1.2% / +0% and +0% / +5%, r03f / r03i)
+          while (m) {
+            const int i = (w << 6) + pop_lowest(m);
+            sphere_candidate(pos, dir, geo[i], i, 0.0001f, t, ind);
+          }
+        }
+      }
+      if (has) {
+        if (PL) plane_pass(P, pos, dir, 0.0001f, t, ind);
+        ++nseg;
+        has = shade(ind, t, pos, dir, hemi, rr, rg, rb, depth, item, false);
+        depth -= 1;
+      }
+    } else if (has) {
       float t;
       int ind = closest_hit_pf(geo, nobj, pos, dir, 0.0001f, t);  // 4-sphere scalar groups (pf2: +0.9%)
       if (PL) plane_pass(P, pos, dir, 0.0001f, t, ind);
@@ -1334,6 +1461,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       has = shade(ind, t, pos, dir, hemi, rr, rg, rb, depth, item, false);
       depth -= 1;
     }
+    if (ABL == 8) tsec[6] += 1;
     lap(3);
   }
   lap(2);
@@ -1382,13 +1510,13 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     if (kind == PRIM_HIT) {
       float4 r0 = prec[lp];
       d = make_float4(r0.w, 0.0f, 0.0f, 1.0f);
-      f_nrm[off] = make_float4(r0.x, r0.y, r0.z, 1.0f);
+      nrm_store(f_nrm, dep_plane(P), off, make_float4(r0.x, r0.y, r0.z, 1.0f));
     } else if (kind == PRIM_MISS) {
       d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      f_nrm[off] = d;
+      nrm_store(f_nrm, dep_plane(P), off, d);
     } else {  // stale: the slot's previous normal / depth (an emissive first hit writes neither)
       d = dep_load(f_dep_prev, dep_plane(P), off);
-      if (f_nrm_prev != f_nrm) f_nrm[off] = f_nrm_prev[off];
+      if (f_nrm_prev != f_nrm) nrm_store(f_nrm, dep_plane(P), off, nrm_load(f_nrm_prev, dep_plane(P), off));
     }
     if (ystop >= 0.0f) d.y = ystop;
     d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
@@ -1409,24 +1537,53 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
 // neighbours read `raw` (slot f before filtering); right iff x+1<W, left iff x>0,
 // up iff y+1<H, down iff y>=2.  Output goes to out_pix (the shim swaps it into slot f).
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, unsigned& visited, unsigned& accepted);
+__device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, unsigned& filtered, unsigned& visited,
+                                           unsigned& accepted);
 
-__device__ __forceinline__ float nbr_weight(f3 n, float nd, float nb, float4 kn, float2 kd) {
-  if (kn.w < 0.001f) return 1.0f;
-  float normal_dot = dot(n, xyz(kn));
+__device__ __forceinline__ float nbr_weight(f3 n, float nd, float nb, const float4* nrm, size_t np, const float4* dep,
+                                            size_t o) {
+  if (nrm_load_w(nrm, np, o) < 0.001f) return 1.0f;  // (its normal xyz and depth are not read)
+  const float2 kd = dep_load_xy(dep, o);
+  float normal_dot = dot(n, nrm_load_xyz(nrm, o));
   float depth_diff = 1.0f - gclamp(fabsf(nd - kd.x), 0.0f, 1.0f);
   float bounces_diff = 1.0f - gclamp(fabsf(nb - kd.y) / 1.7f, 0.0f, 1.0f);
   return normal_dot * depth_diff * bounces_diff + 0.2f;
 }
 
+// XCD-local tile order: workgroups are dealt round-robin to the 8 XCDs (linear block id L on
+// XCD L mod 8), each with its own L2, so in plain row-major order horizontally adjacent tiles
+// sit on different XCDs and every tile's left / right neighbour columns (whole 128-B lines of
+// raw, normals and depth) are fetched into a second L2.  Here the tiles are cut into runs of R
+// consecutive tiles in row-major order and the runs are dealt round-robin to the XCDs, so most
+// left / right neighbour lines were just brought into the tile's own L2 by the tile before it.
+// The host picks R (launch_params: a divisor of gx / 8 when gx is a multiple of 8, so the tile
+// below a tile is on its XCD too; >= 4).  Runs must stay short: every XCD has to take an equal
+// share of every part of the frame, since sky costs far less than ground (one contiguous band
+// per XCD cut the bytes by 19% but made the launch 43% slower; runs of 1/8 row, 11% slower).
+// L -> run (L / 8 / R) * 8 + L mod 8, offset (L / 8) mod R: a bijection on the first multiple
+// of 8R tiles; the rest keep their order.
+__device__ __forceinline__ void xcd_tile(unsigned R, unsigned& bx, unsigned& by) {
+  const unsigned gx = gridDim.x, n = gx * gridDim.y, L = blockIdx.x + blockIdx.y * gx;
+  const unsigned M = R ? n / (8 * R) * (8 * R) : 0;
+  unsigned t = L;
+  if (L < M) {
+    const unsigned j = L >> 3;
+    t = ((j / R) * 8 + (L & 7u)) * R + j % R;
+  }
+  by = t / gx;
+  bx = t - by * gx;
+}
+
 __global__ __launch_bounds__(kBlock) void post_kernel(FrameParams P) {
   int x, y;
-  tile_xy(x, y, P.trace_row0);
+  unsigned bx, by;
+  xcd_tile((unsigned)P.tile_run, bx, by);
+  tile_xy<2, 2>(x, y, P.trace_row0, (int)bx, (int)by);
   const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
-  unsigned visited = 0, accepted = 0;
-  if (active) post_pixel(P, x, y, visited, accepted);
+  unsigned filtered = 0, visited = 0, accepted = 0;
+  if (active) post_pixel(P, x, y, filtered, visited, accepted);
   if (P.counters) {
-    unsigned n = wave_sum(active ? 1u : 0u), v = wave_sum(visited), a = wave_sum(accepted);
+    unsigned n = wave_sum(filtered), v = wave_sum(visited), a = wave_sum(accepted);
     if ((threadIdx.x & 63) == 0) {
       unsigned long long* c = P.counters + ((blockIdx.x * 4 + blockIdx.y * 4 * gridDim.x + (threadIdx.x >> 6)) &
                                             (kCounterSlots - 1));
@@ -1437,14 +1594,16 @@ __global__ __launch_bounds__(kBlock) void post_kernel(FrameParams P) {
   }
 }
 
-__device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, unsigned& visited, unsigned& accepted) {
+__device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, unsigned& filtered, unsigned& visited,
+                                           unsigned& accepted) {
   const int W = P.W, f = P.frame;
   const size_t off = (size_t)(y - P.band_row0) * W + x;
   float4 color = P.raw[off];
-  const float4 cn = P.nrm[off];
-  if (cn.w > 0.99f) {
+  const size_t np = dep_plane(P);  // normals: xyz plane + w plane (nrm_store)
+  if (nrm_load_w(P.nrm, np, off) > 0.99f) {
+    filtered = 1;
     const float2 cd = dep_load_xy(P.dep, off);
-    const f3 nv = xyz(cn);
+    const f3 nv = nrm_load_xyz(P.nrm, off);
     const float nd = cd.x, nb = cd.y;
     float4 acc = color;
     float den = 1.0f;
@@ -1460,7 +1619,7 @@ __device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, u
       float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       if (present) {
         size_t o = (size_t)(yy - P.band_row0) * W + xx;
-        wk = nbr_weight(nv, nd, nb, P.nrm[o], dep_load_xy(P.dep, o));
+        wk = nbr_weight(nv, nd, nb, P.nrm, np, P.dep, o);
         v = P.raw[o];
       }
       acc.x = acc.x + wk * v.x; acc.y = acc.y + wk * v.y;
@@ -1473,9 +1632,9 @@ __device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, u
     float denominator = 0.9f;
     for (int i = 1; i < P.F; ++i) {
       int cf = (f + P.F - i) % P.F;
-      float4 hn = P.hist_nrm[cf][off];
+      const f3 hn = nrm_load_xyz(P.hist_nrm[cf], off);
       const float2 hd = dep_load_xy(P.hist_dep[cf], off);
-      float normal_dot = dot(nv, xyz(hn));
+      float normal_dot = dot(nv, hn);
       float depth_diff = 1.0f - gclamp(fabsf(nd - hd.x), 0.0f, 1.0f);
       float bounces_diff = 1.0f - gclamp(fabsf(nb - hd.y) / 1.7f, 0.0f, 1.0f);
       float coeff = normal_dot * depth_diff * bounces_diff;
@@ -1567,12 +1726,13 @@ size_t tab_lds_bytes(const FrameParams& p) { return (size_t)5 * (p.nobj > 0 ? p.
 // planes (PL).
 template <int SPPC, bool PL>
 inline void launch_batch(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStream_t stream, const FrameParams& q) {
+  constexpr bool GT = RT_GLOBAL_TAIL;  // split tail rounds above kTailMaxObj spheres (global table)
   if (q.mf_n > 0) {  // multi-frame mode-2 launch (never with counters: rt_compute_frames checks)
     g.y = (unsigned)q.mf_n;
     if (tl)
       hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL, true>), g, b, lds, stream, q, q.sph);
     else
-      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, SPPC, false, false, PL, true>), g, b, lds, stream, q, q.sph);
+      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, false, PL, true>), g, b, lds, stream, q, q.sph);
     return;
   }
   if (tl && cnt)
@@ -1580,9 +1740,9 @@ inline void launch_batch(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStrea
   else if (tl)
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL>), g, b, lds, stream, q, q.sph);
   else if (cnt)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, SPPC, false, true, PL>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, true, PL>), g, b, lds, stream, q, q.sph);
   else
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, false, true, SPPC, false, false, PL>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, false, PL>), g, b, lds, stream, q, q.sph);
 }
 
 // The production launch of `program` (rt_kernels.hip's launch_program; the A/B tools library
@@ -1591,11 +1751,22 @@ inline FrameParams launch_params(const FrameParams& p) {
   FrameParams q = p;
   q.sph = p.shapes + sphere_table(p.S);
   q.planes = p.shapes + plane_table(p.S);
+  q.clus = p.shapes + cluster_table(p.S);
+  q.clmask = (const unsigned long long*)(p.shapes + cluster_mask_table(p.S));
   q.b1_min = 1;
   {  // rotation group: the pools of one image row (at least 8)
     const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
     const int ppr = p.W / TP;
     q.pool_rot = ppr >= 8 ? ppr : 8;
+  }
+  {  // post-process XCD runs (xcd_tile): the least R in [4, gx / 16] dividing gx / 8 (a tile row
+    // is a whole number of 8-run rounds, at least two per XCD), else 4; narrow frames: none
+    const int gx = (p.W + 15) / 16;
+    int R = 0;
+    if (gx % 8 == 0)
+      for (int r = 4; r <= gx / 16 && !R; ++r)
+        if ((gx / 8) % r == 0) R = r;
+    q.tile_run = R ? R : (gx >= 32 ? 4 : 0);
   }
   return q;
 }

@@ -91,6 +91,7 @@ struct rt_ctx {
   std::vector<float4> table;   // host copy of the device table (rt::table_vec4 float4)
   bool have_header = false;
   int nplanes = 0;             // planes among simple_shapes[0, nobj)
+  int ncl = 0;                 // AO bounce-ray clusters of the table the next dispatch reads (build_clusters)
   float4* d_batch = nullptr;   // rt_compute_frames: a batch of device table copies (one per frame)
   float4* d_mf_rb = nullptr;   // rt_compute_frames, mode 2: the rand_buffers of a multi-frame launch
   std::vector<float4> batch_host;
@@ -259,6 +260,7 @@ void fill_params(const rt_ctx* c, int frame, rt::FrameParams& p) {
   p.nobj = c->nobj;
   p.S = table_stride(c);
   p.nplanes = c->nplanes;
+  p.ncl = c->ncl;
   p.spp = c->cfg.spp;
   p.inv_spp = 1.0f / (float)c->cfg.spp;
   p.fW = (float)c->cfg.width;
@@ -457,22 +459,47 @@ int resolve_timing(rt_ctx* c) {
   return RT_OK;
 }
 
-// Depth slots are two planes of [band_rows][W] float2, (x, y) then (z, w) (rt_kernels.hip
-// dep_store): converted to / from interleaved [band_rows][W] float4 around the copies.
-void depth_planes_to_vec4(const float* planes, size_t n, float* v) {
-  for (size_t i = 0; i < n; ++i) {
-    v[4 * i + 0] = planes[2 * i];
-    v[4 * i + 1] = planes[2 * i + 1];
-    v[4 * i + 2] = planes[2 * (n + i)];
-    v[4 * i + 3] = planes[2 * (n + i) + 1];
+// Slot layouts on the device (rt_kernels_impl.h): pixels are [band_rows][W] float4; normals are
+// a [band_rows][W] xyz plane (12 B) then a w plane (4 B) (nrm_store); depth is two [band_rows][W]
+// float2 planes, (x, y) then (z, w) (dep_store).  Converted to / from interleaved [band_rows][W]
+// float4 around the copies.
+enum SlotKind { kPixels = 0, kNormals = 1, kDepth = 2 };
+void planes_to_vec4(int kind, const float* planes, size_t n, float* v) {
+  if (kind == kPixels) {
+    std::memcpy(v, planes, n * 16);
+  } else if (kind == kNormals) {
+    for (size_t i = 0; i < n; ++i) {
+      v[4 * i + 0] = planes[3 * i];
+      v[4 * i + 1] = planes[3 * i + 1];
+      v[4 * i + 2] = planes[3 * i + 2];
+      v[4 * i + 3] = planes[3 * n + i];
+    }
+  } else {
+    for (size_t i = 0; i < n; ++i) {
+      v[4 * i + 0] = planes[2 * i];
+      v[4 * i + 1] = planes[2 * i + 1];
+      v[4 * i + 2] = planes[2 * (n + i)];
+      v[4 * i + 3] = planes[2 * (n + i) + 1];
+    }
   }
 }
-void depth_vec4_to_planes(const float* v, size_t n, float* planes) {
-  for (size_t i = 0; i < n; ++i) {
-    planes[2 * i] = v[4 * i + 0];
-    planes[2 * i + 1] = v[4 * i + 1];
-    planes[2 * (n + i)] = v[4 * i + 2];
-    planes[2 * (n + i) + 1] = v[4 * i + 3];
+void vec4_to_planes(int kind, const float* v, size_t n, float* planes) {
+  if (kind == kPixels) {
+    std::memcpy(planes, v, n * 16);
+  } else if (kind == kNormals) {
+    for (size_t i = 0; i < n; ++i) {
+      planes[3 * i] = v[4 * i + 0];
+      planes[3 * i + 1] = v[4 * i + 1];
+      planes[3 * i + 2] = v[4 * i + 2];
+      planes[3 * n + i] = v[4 * i + 3];
+    }
+  } else {
+    for (size_t i = 0; i < n; ++i) {
+      planes[2 * i] = v[4 * i + 0];
+      planes[2 * i + 1] = v[4 * i + 1];
+      planes[2 * (n + i)] = v[4 * i + 2];
+      planes[2 * (n + i) + 1] = v[4 * i + 3];
+    }
   }
 }
 
@@ -682,9 +709,86 @@ int rt_last_hip_error(rt_ctx* c) { return c ? c->last_hip : 0; }
 
 namespace {
 
+// Bounce-ray clusters of the AO kernel's later bounce rounds (rt_kernels_impl.h cluster_may_hit):
+// the spheres among [0, nobj) are cut into spatial groups of at most kClusterSize by recursive
+// median splits of their centres along the widest axis; each cluster is stored as (centre, R)
+// with every member inside the ball: |c_i - centre| + |r_i| <= R (computed in double and
+// rounded up).  Spheres that would inflate a cluster (radius above 8x the median, e.g. a ground
+// sphere) and spheres with non-finite geometry are tested in every round instead (the always
+// mask).  Non-spheres (NaN in the sphere table) are never accepted and are left out entirely.
+// Returns the cluster count, 0 = off (small scenes, more than 256 objects, nothing to cluster).
+constexpr int kClusterSize = 8;
+constexpr int kClusterMinObj = 16;
+int build_clusters(const float4* sph, int nobj, float4* ctab, unsigned long long* cmask) {
+  std::memset(cmask, 0, sizeof(unsigned long long) * (1 + rt::kMaxClusters) * rt::kClusterWords);
+  if (nobj < kClusterMinObj || nobj > 64 * rt::kClusterWords) return 0;
+  std::vector<int> small;
+  std::vector<float> radii;
+  for (int i = 0; i < nobj; ++i) {
+    const float4 g = sph[i];
+    if (g.x != g.x) continue;  // not a sphere (NaN row): never accepted
+    if (std::isfinite(g.x) && std::isfinite(g.y) && std::isfinite(g.z) && std::isfinite(g.w)) radii.push_back(std::fabs(g.w));
+  }
+  if (radii.size() < (size_t)kClusterSize) return 0;
+  std::nth_element(radii.begin(), radii.begin() + radii.size() / 2, radii.end());
+  const double big = 8.0 * radii[radii.size() / 2];
+  for (int i = 0; i < nobj; ++i) {
+    const float4 g = sph[i];
+    if (g.x != g.x) continue;
+    const bool fin = std::isfinite(g.x) && std::isfinite(g.y) && std::isfinite(g.z) && std::isfinite(g.w);
+    if (fin && std::fabs(g.w) <= big) small.push_back(i);
+    else cmask[i >> 6] |= 1ull << (i & 63);  // always tested
+  }
+  // recursive median split into groups of <= kClusterSize
+  std::vector<std::pair<int, int>> groups, work{{0, (int)small.size()}};
+  while (!work.empty()) {
+    auto [a, b] = work.back();
+    work.pop_back();
+    if (b - a <= kClusterSize) {
+      groups.push_back({a, b});
+      continue;
+    }
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (int k = a; k < b; ++k) {
+      const float4 g = sph[small[k]];
+      const double v[3] = {g.x, g.y, g.z};
+      for (int d = 0; d < 3; ++d) lo[d] = std::min(lo[d], v[d]), hi[d] = std::max(hi[d], v[d]);
+    }
+    int ax = 0;
+    for (int d = 1; d < 3; ++d)
+      if (hi[d] - lo[d] > hi[ax] - lo[ax]) ax = d;
+    const int mid = (a + b) / 2;
+    auto key = [&](int i) { const float4 g = sph[i]; return ax == 0 ? g.x : ax == 1 ? g.y : g.z; };
+    std::nth_element(small.begin() + a, small.begin() + mid, small.begin() + b,
+                     [&](int i, int j) { return key(i) < key(j) || (key(i) == key(j) && i < j); });
+    work.push_back({mid, b});
+    work.push_back({a, mid});
+  }
+  if ((int)groups.size() > rt::kMaxClusters) {  // too many groups: test everything every round
+    std::memset(cmask, 0, sizeof(unsigned long long) * rt::kClusterWords);
+    return 0;
+  }
+  int k = 0;
+  for (auto [a, b] : groups) {
+    double cx = 0, cy = 0, cz = 0;
+    for (int q = a; q < b; ++q) cx += sph[small[q]].x, cy += sph[small[q]].y, cz += sph[small[q]].z;
+    const float fx = (float)(cx / (b - a)), fy = (float)(cy / (b - a)), fz = (float)(cz / (b - a));
+    double R = 0.0;
+    for (int q = a; q < b; ++q) {
+      const float4 g = sph[small[q]];
+      const double dx = (double)g.x - fx, dy = (double)g.y - fy, dz = (double)g.z - fz;
+      R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz) + std::fabs((double)g.w));
+      cmask[(size_t)(1 + k) * rt::kClusterWords + (small[q] >> 6)] |= 1ull << (small[q] & 63);
+    }
+    ctab[k] = make_float4(fx, fy, fz, std::nextafter((float)(R * (1.0 + 1e-6)), INFINITY));
+    ++k;
+  }
+  return k;
+}
+
 // Validate a header and pack it into the device table layout (rt::table_vec4 float4 at `tab`:
-// shape tables, sphere table, plane table, rand_buffer); sets nobj / nplanes.
-int pack_header(rt_ctx* c, const float* h, float4* tab, int& nobj, int& nplanes) {
+// shape tables, sphere table, plane table, clusters, rand_buffer); sets nobj / nplanes / ncl.
+int pack_header(rt_ctx* c, const float* h, float4* tab, int& nobj, int& nplanes, int& ncl) {
   const int S = c->cfg.num_shapes, spp = c->cfg.spp;
   const float mz = h[RT_HDR_MODE * 4 + 2];
   if (!(mz >= 0.0f && mz < (float)(S + 1))) return RT_E_INVAL;  // int(mode.z) must be in [0, S]
@@ -718,6 +822,7 @@ int pack_header(rt_ctx* c, const float* h, float4* tab, int& nobj, int& nplanes)
   }
   std::memcpy(tab + rt::rand_table(Sc), h + rt_off_rand(S) / 4, (size_t)2 * spp * sizeof(float4));
   nplanes = np;
+  ncl = build_clusters(sph, nobj, tab + rt::cluster_table(Sc), (unsigned long long*)(tab + rt::cluster_mask_table(Sc)));
   return RT_OK;
 }
 
@@ -730,13 +835,13 @@ int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
   const int S = c->cfg.num_shapes, spp = c->cfg.spp;
   if (bytes != rt_header_bytes(S, spp)) return RT_E_INVAL;
   const float* h = (const float*)header;
-  int nobj = 0, np = 0;
+  int nobj = 0, np = 0, ncl = 0;
   {
     const float mz = h[RT_HDR_MODE * 4 + 2];
     if (!(mz >= 0.0f && mz < (float)(S + 1))) return RT_E_INVAL;
   }
   std::memcpy(c->header.data(), header, bytes);
-  int rc = pack_header(c, h, c->table.data(), nobj, np);
+  int rc = pack_header(c, h, c->table.data(), nobj, np, ncl);
   if (rc != RT_OK) return rc;
   RT_HIP(c, hipSetDevice(c->device));
   // pipelined: into the header copy of the next frame, on its AO stream (ordered after the AO
@@ -753,6 +858,7 @@ int rt_upload_header(rt_ctx* c, const void* header, size_t bytes) {
   c->d_rb = c->d_rb_buf[hc];
   c->nobj = nobj;
   c->nplanes = np;
+  c->ncl = ncl;
   c->have_header = true;
   return RT_OK;
 }
@@ -899,11 +1005,11 @@ int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint
   const size_t hf = bytes / sizeof(float);
   for (int k0 = 0; k0 < n; k0 += kBatch) {
     const int m = std::min(kBatch, n - k0);
-    std::vector<int> nobj(m), npl(m), slot(m);
+    std::vector<int> nobj(m), npl(m), ncl(m), slot(m);
     int f = frame;
     for (int j = 0; j < m; ++j) {
       int rc = update(k0 + j, f);
-      if (rc == RT_OK) rc = pack_header(c, header, c->batch_host.data() + (size_t)j * tv, nobj[j], npl[j]);
+      if (rc == RT_OK) rc = pack_header(c, header, c->batch_host.data() + (size_t)j * tv, nobj[j], npl[j], ncl[j]);
       if (rc != RT_OK) return rc;
       std::memcpy(c->batch_hdr.data() + (size_t)j * hf, header, bytes);  // camera / light of frame j
       slot[j] = f;
@@ -916,6 +1022,7 @@ int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint
       c->d_rb = c->d_shapes + rt::rand_table(Sc);
       c->nobj = nobj[j];
       c->nplanes = npl[j];
+      c->ncl = ncl[j];
       c->have_header = true;
       std::memcpy(c->header.data(), c->batch_hdr.data() + (size_t)j * hf, bytes);  // launch parameters
       frame = rt_dispatch(c, mode, slot[j]);
@@ -938,23 +1045,18 @@ int rt_download(rt_ctx* c, float* pixels, float* normals, float* depth, float* i
   const int F = c->cfg.num_frames;
   const size_t slot = slot_elems(c);
   const size_t ref_slot = (size_t)c->cfg.width * c->own_rows * 4;
-  std::vector<float> tmp(slot * 4), tmp2(depth ? slot * 4 : 0);
+  std::vector<float> tmp(slot * 4), tmp2(slot * 4);
   int rc = join(c);
   if (rc == RT_OK) rc = sync_all(c);
   if (rc != RT_OK) return rc;
   for (int f = 0; f < F; ++f) {
-    if (pixels) {
-      RT_HIP(c, hipMemcpy(tmp.data(), c->pix[c->pix_slot[f]], slot * 16, hipMemcpyDeviceToHost));
-      dev_to_ref(c, tmp.data(), pixels + f * ref_slot);
-    }
-    if (normals) {
-      RT_HIP(c, hipMemcpy(tmp.data(), c->nrm[c->nrm_slot[f]], slot * 16, hipMemcpyDeviceToHost));
-      dev_to_ref(c, tmp.data(), normals + f * ref_slot);
-    }
-    if (depth) {
-      RT_HIP(c, hipMemcpy(tmp2.data(), c->dep[c->dep_slot[f]], slot * 16, hipMemcpyDeviceToHost));
-      depth_planes_to_vec4(tmp2.data(), slot, tmp.data());
-      dev_to_ref(c, tmp.data(), depth + f * ref_slot);
+    struct { float* dst; const float4* src; } items[3] = {
+        {pixels, c->pix[c->pix_slot[f]]}, {normals, c->nrm[c->nrm_slot[f]]}, {depth, c->dep[c->dep_slot[f]]}};
+    for (int k = 0; k < 3; ++k) {
+      if (!items[k].dst) continue;
+      RT_HIP(c, hipMemcpy(tmp2.data(), items[k].src, slot * 16, hipMemcpyDeviceToHost));
+      planes_to_vec4(k, tmp2.data(), slot, tmp.data());
+      dev_to_ref(c, tmp.data(), items[k].dst + f * ref_slot);
     }
   }
   if (image)
@@ -977,14 +1079,24 @@ int rt_download_rect(rt_ctx* c, int x0, int x1, int y0, int y1, float* pixels, f
   auto rect = [&](const float4* base, int r0) {  // rows [r0, r0 + h) of a [rows][W] device array
     return hipMemcpy2D(tmp.data(), row, base + (size_t)r0 * W + x0, pitch, row, h, hipMemcpyDeviceToHost);
   };
-  // a depth slot's rect: the (x, y) and (z, w) planes, interleaved into tmp
-  const size_t n = slot_elems(c), pitch2 = (size_t)W * sizeof(float2), row2 = (size_t)w * sizeof(float2);
-  std::vector<float2> t0((size_t)w * h), t1((size_t)w * h);
-  auto depth_rect = [&](const float4* base, int r0) -> hipError_t {
-    const float2* p = (const float2*)base + (size_t)r0 * W + x0;
-    hipError_t e = hipMemcpy2D(t0.data(), row2, p, pitch2, row2, h, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy2D(t1.data(), row2, p + n, pitch2, row2, h, hipMemcpyDeviceToHost);
-    for (size_t i = 0; i < t0.size(); ++i) tmp[i] = make_float4(t0[i].x, t0[i].y, t1[i].x, t1[i].y);
+  // a plane-split slot's rect: plane a (ea floats per pixel) then plane b (4 - ea floats per
+  // pixel, starting ea * n floats into the slot), interleaved into tmp
+  const size_t n = slot_elems(c);
+  std::vector<float> ta((size_t)w * h * 3), tb((size_t)w * h * 3);
+  auto split_rect = [&](const float4* base, int r0, int ea) -> hipError_t {
+    const int eb = 4 - ea;
+    const float* pa = (const float*)base + ((size_t)r0 * W + x0) * ea;
+    const float* pb = (const float*)base + ea * n + ((size_t)r0 * W + x0) * eb;
+    hipError_t e = hipMemcpy2D(ta.data(), (size_t)w * ea * 4, pa, (size_t)W * ea * 4, (size_t)w * ea * 4, h,
+                               hipMemcpyDeviceToHost);
+    if (e == hipSuccess)
+      e = hipMemcpy2D(tb.data(), (size_t)w * eb * 4, pb, (size_t)W * eb * 4, (size_t)w * eb * 4, h,
+                      hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < (size_t)w * h; ++i) {
+      float* o = (float*)&tmp[i];
+      for (int q = 0; q < ea; ++q) o[q] = ta[i * ea + q];
+      for (int q = 0; q < eb; ++q) o[ea + q] = tb[i * eb + q];
+    }
     return e;
   };
   for (int f = 0; f < F; ++f) {
@@ -993,7 +1105,7 @@ int rt_download_rect(rt_ctx* c, int x0, int x1, int y0, int y1, float* pixels, f
     for (int k = 0; k < 3; ++k) {
       auto& it = items[k];
       if (!it.dst) continue;
-      RT_HIP(c, k == 2 ? depth_rect(it.src, y0 - c->band0) : rect(it.src, y0 - c->band0));
+      RT_HIP(c, k == kPixels ? rect(it.src, y0 - c->band0) : split_rect(it.src, y0 - c->band0, k == kNormals ? 3 : 2));
       float* out = it.dst + (size_t)f * w * h * 4;  // [w][h] vec4, y fastest (reference layout)
       for (int x = 0; x < w; ++x)
         for (int r = 0; r < h; ++r) std::memcpy(out + ((size_t)x * h + r) * 4, &tmp[(size_t)r * w + x], 16);
@@ -1012,7 +1124,7 @@ int rt_upload_gbuffer(rt_ctx* c, const float* pixels, const float* normals, cons
   const int F = c->cfg.num_frames;
   const size_t slot = slot_elems(c);
   const size_t ref_slot = (size_t)c->cfg.width * c->own_rows * 4;
-  std::vector<float> tmp(slot * 4), tmp2(depth ? slot * 4 : 0);
+  std::vector<float> tmp(slot * 4), tmp2(slot * 4);
   int rc = join(c);
   if (rc == RT_OK) rc = sync_all(c);
   if (rc != RT_OK) return rc;
@@ -1022,12 +1134,11 @@ int rt_upload_gbuffer(rt_ctx* c, const float* pixels, const float* normals, cons
     for (int k = 0; k < 3; ++k) {
       auto& it = items[k];
       if (!it.src) continue;
-      const bool dp = k == 2;  // depth slots hold two float2 planes
-      RT_HIP(c, hipMemcpy(dp ? tmp2.data() : tmp.data(), it.dst, slot * 16, hipMemcpyDeviceToHost));  // keep halo rows
-      if (dp) depth_planes_to_vec4(tmp2.data(), slot, tmp.data());
+      RT_HIP(c, hipMemcpy(tmp2.data(), it.dst, slot * 16, hipMemcpyDeviceToHost));  // keep halo rows
+      planes_to_vec4(k, tmp2.data(), slot, tmp.data());
       ref_to_dev(c, it.src + f * ref_slot, tmp.data());
-      if (dp) depth_vec4_to_planes(tmp.data(), slot, tmp2.data());
-      RT_HIP(c, hipMemcpy(it.dst, dp ? tmp2.data() : tmp.data(), slot * 16, hipMemcpyHostToDevice));
+      vec4_to_planes(k, tmp.data(), slot, tmp2.data());
+      RT_HIP(c, hipMemcpy(it.dst, tmp2.data(), slot * 16, hipMemcpyHostToDevice));
     }
   }
   return RT_OK;

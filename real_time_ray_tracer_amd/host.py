@@ -318,7 +318,7 @@ class Renderer:
         out = (C.c_uint64 * 8)()
         self._c(self._lib.rt_read_counters(self.ctx, out, int(reset)), "rt_read_counters")
         return {"samples": out[0], "segments": out[1], "shadow_rays": out[2], "tests": out[3],
-                "executed_lane_tests": out[4], "post_pixels": out[5], "history_read": out[6],
+                "executed_lane_tests": out[4], "filtered_pixels": out[5], "history_read": out[6],
                 "history_accepted": out[7]}
 
     def read_row_counters(self, reset: bool = True) -> np.ndarray:

@@ -182,3 +182,42 @@ def test_pool_rotation_spreads_columns_over_xcds():
     for xcd in range(8):
         res = {pool_of_block(b, 8 * Q, Q) % Q % 8 for b in range(8 * Q) if b % 8 == xcd}
         assert res == set(range(8))
+
+
+def post_tile_of_block(L: int, gx: int, gy: int, R: int) -> int:
+    """post_kernel's workgroup -> tile map (rt_kernels_impl.h xcd_tile): runs of R tiles dealt
+    round-robin to the 8 XCDs; a trailing partial round keeps its order."""
+    n = gx * gy
+    M = n // (8 * R) * (8 * R) if R else 0
+    if L >= M:
+        return L
+    j = L >> 3
+    return ((j // R) * 8 + (L & 7)) * R + j % R
+
+
+def post_tile_run(W: int) -> int:
+    """launch_params' choice of R for the post-process (the least R in [4, gx/16] dividing gx/8)."""
+    gx = (W + 15) // 16
+    if gx % 8 == 0:
+        for r in range(4, gx // 16 + 1):
+            if (gx // 8) % r == 0:
+                return r
+    return 4 if gx >= 32 else 0
+
+
+@pytest.mark.parametrize("W,H", [(3840, 2160), (1920, 1080), (7680, 4320), (440, 330), (640, 480), (200, 150)])
+def test_post_tile_order_is_a_bijection_with_xcd_local_neighbours(W, H):
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    R = post_tile_run(W)
+    m = [post_tile_of_block(L, gx, gy, R) for L in range(gx * gy)]
+    assert sorted(m) == list(range(gx * gy))
+    if R and gx % 8 == 0 and (gx // R) % 8 == 0:
+        xcd = {t: L % 8 for L, t in enumerate(m)}
+        full = gx * gy // (8 * R) * (8 * R)
+        # the tile below each tile of a full round is on the same XCD (vertical neighbour lines)
+        same = [xcd[t] == xcd[t - gx] for t in range(gx, full)]
+        assert all(same)
+        # and every XCD takes the same number of tiles from every tile row
+        for row in range(min(gy, full // gx)):
+            counts = [sum(1 for c in range(gx) if xcd[row * gx + c] == k) for k in range(8)]
+            assert len(set(counts)) == 1

@@ -3,6 +3,7 @@
 // the experimental / superseded ones, selected per launch by environment switches read by
 // tools/ab.py, tools/sections.py and tools/variant_counters.py:
 //   RTRT_AO_VARIANT  AO kernel variant (see ab_launch_ao), RTRT_B1_MIN, RTRT_POOL_ROT=0,
+//   RTRT_NO_CLUSTERS=1  the AO bounce rounds without the cluster cull,
 //   RTRT_GENERAL=1   every program on the unculled LDS-table kernels,
 //   RTRT_HY_ABL      hybrid timing ablations, RTRT_HY_BLK hybrid block shapes.
 // Anything not selected runs the production launch (launch_production).
@@ -126,15 +127,15 @@ __global__ __launch_bounds__(kBlock) void ao_kernel(FrameParams P, const float4*
   float4 d;
   if (kind == PRIM_HIT) {
     d = make_float4(t0, 0.0f, 0.0f, 1.0f);
-    P.nrm[off] = make_float4(n0.x, n0.y, n0.z, 1.0f);
+    nrm_store(P.nrm, dep_plane(P), off, make_float4(n0.x, n0.y, n0.z, 1.0f));
   } else if (kind == PRIM_MISS) {
     d = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    P.nrm[off] = d;
+    nrm_store(P.nrm, dep_plane(P), off, d);
   } else {
     // stale: sample 0 hit an emissive shape first (no g-buffer write): the slot keeps its
     // previous normal and depth (read from the slot's previous buffers when pipelined)
     d = dep_load(P.dep_prev, dep_plane(P), off);
-    if (P.nrm_prev != P.nrm) P.nrm[off] = P.nrm_prev[off];
+    if (P.nrm_prev != P.nrm) nrm_store(P.nrm, dep_plane(P), off, nrm_load(P.nrm_prev, dep_plane(P), off));
   }
   if (ystop >= 0.0f) d.y = ystop;
   d.x = d.x / fa; d.y = d.y / fa; d.z = d.z / fa; d.w = d.w / fa;
@@ -156,6 +157,7 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
   const int variant = ev ? atoi(ev) : 7;
   const char* eb = getenv("RTRT_B1_MIN");
   q.b1_min = eb ? atoi(eb) : 1;
+  if (const char* en = getenv("RTRT_NO_CLUSTERS"); en && atoi(en) == 1) q.ncl = 0;  // A/B: no bounce-ray cluster cull
   const char* er = getenv("RTRT_POOL_ROT");
   if (er && atoi(er) == 0) q.pool_rot = 0;  // A/B: pools in plain row order
   const char* eg = getenv("RTRT_GENERAL");
@@ -197,6 +199,8 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2>), g, b, psh, stream, q, q.sph);
   else if (variant == 96 && tl && p.spp == 16)  // section clocks, first bounce split in 3
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 6, true, true, 16, true>), g, b, psh, stream, q, q.sph);
+  else if (variant == 98 && tl && p.spp == 16)  // section clocks, split tail rounds apart from full rounds
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 8, true, true, 16, true>), g, b, psh, stream, q, q.sph);
   else if (variant == 97 && tl && p.spp == 16)  // first-bounce / bounce-round event counts
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 7, true, true, 16, true>), g, b, psh, stream, q, q.sph);
   else if (variant == 93 && tl && p.spp == 16)  // section clocks of the production kernel

@@ -5,6 +5,7 @@
     python tools/sections.py --config d --frames 3
     python tools/sections.py --config d --variant 96   # the first bounce split into cull / survivors / shade
     python tools/sections.py --config d --variant 97   # event counts: first-bounce survivors, bounce-round tails
+    python tools/sections.py --config d --variant 98   # full bounce rounds and split tail rounds apart
 """
 import argparse
 import os
@@ -41,7 +42,7 @@ def main():
         r.upload_header(h)
         f = r.dispatch(2 if mode == 1 else mode, f)  # AO pass only: counters 5..7 are the kernel's
     c = r.read_counters()
-    keys = ["samples", "segments", "shadow_rays", "tests", "executed_lane_tests", "post_pixels", "history_read",
+    keys = ["samples", "segments", "shadow_rays", "tests", "executed_lane_tests", "filtered_pixels", "history_read",
             "history_accepted"]
     if a.variant == "97":
         v = [c[k] for k in keys]
@@ -50,6 +51,15 @@ def main():
         print(f"  survivor iterations with any pre-test pass {v[1] / max(v[0], 1):.3f}, with any del >= 0 among "
               f"the passing lanes {v[2] / max(v[0], 1):.3f}; lanes passing per iteration {v[3] / max(v[0], 1):.2f}")
         print(f"bounce rounds: {v[6]} sphere iterations, any live lane del >= 0 in {v[7] / max(v[6], 1):.3f}")
+        return
+    if a.variant == "98":
+        names = ["cull setup", "prepare (primary + first shade)", "hand-out / regeneration", "full bounce rounds",
+                 "first bounce (batched) + combine + stores", "split tail rounds"]
+        v = [c[k] for k in keys]
+        tot = sum(v[:6])
+        for n, x in zip(names, v[:6]):
+            print(f"{n:42s} {x / 1e9:9.3f} Gclk  {100 * x / tot:5.1f}%")
+        print(f"full rounds {v[6]}, split tail rounds {v[7]}")
         return
     if a.variant == "96":
         names = ["cull setup", "prepare (primary + first shade)", "hand-out / regeneration", "bounce test + shade",
@@ -63,7 +73,7 @@ def main():
     tot = sum(vals)
     for n, v in zip(NAMES, vals):
         print(f"{n:34s} {v / 1e9:9.3f} Gclk  {100 * v / tot:5.1f}%")
-    rounds, sum_ncull, prepares = c["post_pixels"], c["history_read"], c["history_accepted"]
+    rounds, sum_ncull, prepares = c["filtered_pixels"], c["history_read"], c["history_accepted"]
     b1_surv, sum_ncull = sum_ncull >> 24, sum_ncull & ((1 << 24) - 1)
     print(f"batched first bounce: {b1_surv / max(prepares, 1):.2f} spheres tested per prepared batch (of {S})")
     print(f"bounce rounds {rounds}  prepares {prepares}  mean culled primary set {sum_ncull / max(prepares, 1):.2f}")
