@@ -506,6 +506,22 @@ def main():
     progs = {1: [1, 2], 2: [3], 3: [4], 4: [5]}[mode]
     kstats = {p: rend.kernel_stats(p) for p in progs}
 
+    # ---- the reference's dispatch shape for the batched modes: one launch and one image write
+    # per frame (rt_set_frame_batch(1)), the same frames through the same C++ loop, wall clock --
+    per_frame = None
+    if host_loop and mode in (2, 3, 4):
+        rend.set_frame_batch(1)
+        torch.cuda.synchronize()
+        t0p = time.perf_counter()
+        state["frame"] = rend.compute_frames(header, mode, state["frame"], args.steps, 7000 + warm, False)
+        torch.cuda.synchronize()
+        pf_s = (time.perf_counter() - t0p) / args.steps
+        rend.set_frame_batch(32)
+        per_frame = {"ms_per_step": round(pf_s * 1e3, 4),
+                     "value": round(W * H * (spp if mode in (1, 2) else 1) / pf_s / 1e6, 2),
+                     "dispatch": "one launch and one image write per frame (rt_set_frame_batch(1)), C++ frame loop, "
+                                 "wall clock over the same number of frames"}
+
     # ---- standalone kernel times (two frames, not overlapped) and work counters (two more,
     # un-timed) on the timed frames' inputs -------------------------------------------------
     if gather is not None:
@@ -630,6 +646,11 @@ def main():
             "host_backpressure_ms_per_step": round(host_wait_ms / args.steps, 4),
             "build": binfo,
         }
+        if per_frame is not None:
+            out["per_frame_dispatch"] = per_frame
+            out["dispatch"] = ("batched: up to 8 frames per launch, each frame writing its own ring slot and the "
+                               "launch's last frame the image (value and ms_per_step); per_frame_dispatch has the "
+                               "reference's one-launch-per-frame shape")
         if balance_info is not None:
             sm = strip_ms.cpu().tolist()
             balance_info.update({"strip_ms": [round(t, 4) for t in sm], "imbalance": round(imbalance(sm), 4)})

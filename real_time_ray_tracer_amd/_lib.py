@@ -56,6 +56,7 @@ SIGNATURES = {
     "rt_run_program": (C.c_int, [_ctx, C.c_int, C.c_int]),
     "rt_dispatch": (C.c_int, [_ctx, C.c_int, C.c_int]),
     "rt_compute_frames": (C.c_int, [_ctx, _fp, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int]),
+    "rt_set_frame_batch": (C.c_int, [_ctx, C.c_int]),
     "rt_download": (C.c_int, [_ctx, _fp, _fp, _fp, _fp]),
     "rt_download_rect": (C.c_int, [_ctx, C.c_int, C.c_int, C.c_int, C.c_int, _fp, _fp, _fp, _fp]),
     "rt_upload_gbuffer": (C.c_int, [_ctx, _fp, _fp, _fp]),

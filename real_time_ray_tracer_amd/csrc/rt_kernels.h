@@ -97,6 +97,18 @@ enum KernelId { K_AOP = 1, K_POST = 2, K_AO = 3, K_PHONG = 4, K_HYBRID = 5 };
 // entries of the sphere table.  Returns hipSuccess or the launch error.
 hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream);
 
+// g-buffer layout conversion between the reference's [F][W][R] vec4 (x-major, y fastest:
+// src/main.cpp:49-85 over a context's R rows) and the device slots of one array kind (0 pixels:
+// [band_rows][W] float4; 1 normals: xyz plane + w plane; 2 depth: (x, y) plane + (z, w) plane),
+// rows r0 .. r0 + R - 1 of the band; n = band_rows * W.  to_ref: slots -> ref, else ref -> slots.
+struct GbufXfer {
+  int W, R, r0, F, kind, to_ref;
+  size_t n;
+  float4* ref;
+  float4* slot[kMaxFrames];
+};
+hipError_t launch_gbuf_convert(const GbufXfer& x, hipStream_t stream);
+
 // Device math self-test (rt_selftest_math).
 hipError_t launch_selftest(int fn, const float* d_in, float* d_out, size_t n, hipStream_t stream);
 

@@ -14,4 +14,6 @@ hipError_t launch_selftest(int fn, const float* d_in, float* d_out, size_t n, hi
   return launch_selftest_impl(fn, d_in, d_out, n, stream);
 }
 
+hipError_t launch_gbuf_convert(const GbufXfer& x, hipStream_t stream) { return launch_gbuf_convert_impl(x, stream); }
+
 }  // namespace rt

@@ -1745,6 +1745,36 @@ inline void launch_batch(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStrea
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, false, PL>), g, b, lds, stream, q, q.sph);
 }
 
+// g-buffer layout conversion (rt_download / rt_upload_gbuffer, the host-buffer path of
+// compute_one_shader / compute_two_shaders): one thread per reference vec4, reference side
+// coalesced.
+__global__ __launch_bounds__(256) void gbuf_convert_kernel(GbufXfer x) {
+  const size_t total = (size_t)x.F * x.W * x.R;
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const size_t wr = (size_t)x.W * x.R;
+  const int f = (int)(idx / wr);
+  const size_t rem = idx - (size_t)f * wr;
+  const int xx = (int)(rem / x.R), r = (int)(rem - (size_t)xx * x.R);
+  const size_t o = (size_t)(x.r0 + r) * x.W + xx;
+  float4* base = x.slot[f];
+  if (x.to_ref) {
+    x.ref[idx] = x.kind == 0 ? base[o] : x.kind == 1 ? nrm_load(base, x.n, o) : dep_load(base, x.n, o);
+  } else {
+    const float4 v = x.ref[idx];
+    if (x.kind == 0) base[o] = v;
+    else if (x.kind == 1) nrm_store(base, x.n, o, v);
+    else dep_store(base, x.n, o, v);
+  }
+}
+
+inline hipError_t launch_gbuf_convert_impl(const GbufXfer& x, hipStream_t stream) {
+  const size_t total = (size_t)x.F * x.W * x.R;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(gbuf_convert_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, x);
+  return hipGetLastError();
+}
+
 // The production launch of `program` (rt_kernels.hip's launch_program; the A/B tools library
 // falls back to it): q = p with the derived table pointers and launch constants.
 inline FrameParams launch_params(const FrameParams& p) {

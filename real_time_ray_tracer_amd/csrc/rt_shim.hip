@@ -92,11 +92,13 @@ struct rt_ctx {
   bool have_header = false;
   int nplanes = 0;             // planes among simple_shapes[0, nobj)
   int ncl = 0;                 // AO bounce-ray clusters of the table the next dispatch reads (build_clusters)
+  float4* d_xfer = nullptr;    // rt_download / rt_upload_gbuffer: one array in the reference layout [F][W][R]
   float4* d_batch = nullptr;   // rt_compute_frames: a batch of device table copies (one per frame)
   float4* d_mf_rb = nullptr;   // rt_compute_frames, mode 2: the rand_buffers of a multi-frame launch
   std::vector<float4> batch_host;
   std::vector<float> batch_hdr;  // the batch's host headers (camera, light: launch parameters)
   int nobj = 0;
+  int mf_max = rt::kMaxBatch;  // rt_compute_frames: most frames per launch (rt_set_frame_batch)
   Stage stage[kStageSlots];
   int stage_next = 0;
   // timing
@@ -200,6 +202,7 @@ void free_all(rt_ctx* c) {
   }
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->d_batch) (void)hipFree(c->d_batch);
+  if (c->d_xfer) (void)hipFree(c->d_xfer);
   if (c->d_mf_rb) (void)hipFree(c->d_mf_rb);
   if (c->d_row_counters) (void)hipFree(c->d_row_counters);
   for (auto e : {c->ev_ao, c->ev_join, c->ev_seq})
@@ -461,60 +464,30 @@ int resolve_timing(rt_ctx* c) {
 
 // Slot layouts on the device (rt_kernels_impl.h): pixels are [band_rows][W] float4; normals are
 // a [band_rows][W] xyz plane (12 B) then a w plane (4 B) (nrm_store); depth is two [band_rows][W]
-// float2 planes, (x, y) then (z, w) (dep_store).  Converted to / from interleaved [band_rows][W]
-// float4 around the copies.
+// float2 planes, (x, y) then (z, w) (dep_store).
 enum SlotKind { kPixels = 0, kNormals = 1, kDepth = 2 };
-void planes_to_vec4(int kind, const float* planes, size_t n, float* v) {
-  if (kind == kPixels) {
-    std::memcpy(v, planes, n * 16);
-  } else if (kind == kNormals) {
-    for (size_t i = 0; i < n; ++i) {
-      v[4 * i + 0] = planes[3 * i];
-      v[4 * i + 1] = planes[3 * i + 1];
-      v[4 * i + 2] = planes[3 * i + 2];
-      v[4 * i + 3] = planes[3 * n + i];
-    }
-  } else {
-    for (size_t i = 0; i < n; ++i) {
-      v[4 * i + 0] = planes[2 * i];
-      v[4 * i + 1] = planes[2 * i + 1];
-      v[4 * i + 2] = planes[2 * (n + i)];
-      v[4 * i + 3] = planes[2 * (n + i) + 1];
-    }
-  }
-}
-void vec4_to_planes(int kind, const float* v, size_t n, float* planes) {
-  if (kind == kPixels) {
-    std::memcpy(planes, v, n * 16);
-  } else if (kind == kNormals) {
-    for (size_t i = 0; i < n; ++i) {
-      planes[3 * i] = v[4 * i + 0];
-      planes[3 * i + 1] = v[4 * i + 1];
-      planes[3 * i + 2] = v[4 * i + 2];
-      planes[3 * n + i] = v[4 * i + 3];
-    }
-  } else {
-    for (size_t i = 0; i < n; ++i) {
-      planes[2 * i] = v[4 * i + 0];
-      planes[2 * i + 1] = v[4 * i + 1];
-      planes[2 * (n + i)] = v[4 * i + 2];
-      planes[2 * (n + i) + 1] = v[4 * i + 3];
-    }
-  }
-}
 
-// device slot [band_rows][W] float4 (own rows) <-> reference [W][R] vec4
-void dev_to_ref(const rt_ctx* c, const float* slot, float* ref) {
-  const int W = c->cfg.width, R = c->own_rows, r0 = c->own0 - c->band0;
-  for (int x = 0; x < W; ++x)
-    for (int r = 0; r < R; ++r)
-      std::memcpy(ref + ((size_t)x * R + r) * 4, slot + ((size_t)(r0 + r) * W + x) * 4, 16);
+// The g-buffer in the reference layout ([F][W][R] vec4, y fastest) goes through one device array
+// of that layout: a conversion kernel (rt::launch_gbuf_convert) between it and the slot layouts,
+// and one copy of exactly the caller's bytes (no host-side transposes).
+int xfer_buffer(rt_ctx* c) {
+  if (!c->d_xfer) RT_HIP(c, hipMalloc(&c->d_xfer, (size_t)c->cfg.num_frames * c->cfg.width * c->own_rows * sizeof(float4)));
+  return RT_OK;
 }
-void ref_to_dev(const rt_ctx* c, const float* ref, float* slot) {
-  const int W = c->cfg.width, R = c->own_rows, r0 = c->own0 - c->band0;
-  for (int x = 0; x < W; ++x)
-    for (int r = 0; r < R; ++r)
-      std::memcpy(slot + ((size_t)(r0 + r) * W + x) * 4, ref + ((size_t)x * R + r) * 4, 16);
+rt::GbufXfer xfer_desc(const rt_ctx* c, int kind, int to_ref) {
+  rt::GbufXfer x{};
+  x.W = c->cfg.width;
+  x.R = c->own_rows;
+  x.r0 = c->own0 - c->band0;
+  x.F = c->cfg.num_frames;
+  x.kind = kind;
+  x.to_ref = to_ref;
+  x.n = slot_elems(c);
+  x.ref = c->d_xfer;
+  const std::vector<float4*>& bufs = kind == kPixels ? c->pix : kind == kNormals ? c->nrm : c->dep;
+  const std::vector<int>& map = kind == kPixels ? c->pix_slot : kind == kNormals ? c->nrm_slot : c->dep_slot;
+  for (int f = 0; f < x.F; ++f) x.slot[f] = bufs[map[f]];
+  return x;
 }
 
 }  // namespace
@@ -920,7 +893,7 @@ int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint
     if (!(mz >= 0.0f && mz < (float)(S + 1))) return RT_E_INVAL;
     return rt_set_mode(header, slot, (int)mz);
   };
-  if ((mode == RT_MODE_PHONG || mode == RT_MODE_PHONG_REFL) && n >= 2) {
+  if ((mode == RT_MODE_PHONG || mode == RT_MODE_PHONG_REFL) && n >= 2 && c->mf_max > 1) {
     // Modes 3/4: the per-frame host update moves only the light (and mode.y), so the shape
     // table is uploaded once and up to kMaxBatch frames go in one multi-frame launch with their
     // lights (run_program_mf).  Every frame writes its own colour slot, as frame-by-frame calls
@@ -941,7 +914,7 @@ int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint
     const int prog = mode == RT_MODE_PHONG ? RT_PROG_P_COMPUTE : RT_PROG_H_COMPUTE;
     // at most F frames per launch: each colour slot is written by one frame of a launch (frames
     // k and k + F of one launch would race for slot k % F)
-    const int mb = std::min(rt::kMaxBatch, c->cfg.num_frames);
+    const int mb = std::min(std::min(rt::kMaxBatch, c->mf_max), c->cfg.num_frames);
     for (int k0 = 0; k0 < n; k0 += mb) {
       const int m = std::min(mb, n - k0);
       int rc = run_program_mf(c, prog, slots[k0], m, lights.data() + k0);
@@ -949,7 +922,7 @@ int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint
     }
     return f;
   }
-  if (mode == RT_MODE_AO && n >= 2 && !c->counting && !c->row_counting) {
+  if (mode == RT_MODE_AO && n >= 2 && !c->counting && !c->row_counting && c->mf_max > 1) {
     // Mode 2: the per-frame host update replaces only rand_buffer (fill_rand_buffer,
     // src/main.cpp:535-539) and mode.y, so the shape table is uploaded once and up to F frames
     // go in one launch, each with its own rand_buffer (run_program_mf).
@@ -967,7 +940,7 @@ int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint
     }
     RT_HIP(c, hipSetDevice(c->device));
     if (!c->d_mf_rb) RT_HIP(c, hipMalloc(&c->d_mf_rb, (size_t)rt::kMaxBatch * nrb * sizeof(float4)));
-    const int mb = std::min(rt::kMaxBatch, c->cfg.num_frames);
+    const int mb = std::min(std::min(rt::kMaxBatch, c->mf_max), c->cfg.num_frames);
     for (int k0 = 0; k0 < n; k0 += mb) {
       const int m = std::min(mb, n - k0);
       int rc = staged_copy(c, c->d_mf_rb, &rbs[(size_t)k0 * nrb], (size_t)m * nrb * sizeof(float4), c->stream);
@@ -1039,28 +1012,30 @@ int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint
   return frame;
 }
 
+int rt_set_frame_batch(rt_ctx* c, int max_frames) {
+  if (!c || max_frames < 1) return RT_E_INVAL;
+  c->mf_max = std::min(max_frames, rt::kMaxBatch);
+  return RT_OK;
+}
+
 int rt_download(rt_ctx* c, float* pixels, float* normals, float* depth, float* image) {
   if (!c) return RT_E_INVAL;
   RT_HIP(c, hipSetDevice(c->device));
-  const int F = c->cfg.num_frames;
-  const size_t slot = slot_elems(c);
-  const size_t ref_slot = (size_t)c->cfg.width * c->own_rows * 4;
-  std::vector<float> tmp(slot * 4), tmp2(slot * 4);
   int rc = join(c);
   if (rc == RT_OK) rc = sync_all(c);
+  if (rc == RT_OK && (pixels || normals || depth)) rc = xfer_buffer(c);
   if (rc != RT_OK) return rc;
-  for (int f = 0; f < F; ++f) {
-    struct { float* dst; const float4* src; } items[3] = {
-        {pixels, c->pix[c->pix_slot[f]]}, {normals, c->nrm[c->nrm_slot[f]]}, {depth, c->dep[c->dep_slot[f]]}};
-    for (int k = 0; k < 3; ++k) {
-      if (!items[k].dst) continue;
-      RT_HIP(c, hipMemcpy(tmp2.data(), items[k].src, slot * 16, hipMemcpyDeviceToHost));
-      planes_to_vec4(k, tmp2.data(), slot, tmp.data());
-      dev_to_ref(c, tmp.data(), items[k].dst + f * ref_slot);
-    }
+  const size_t bytes = (size_t)c->cfg.num_frames * c->cfg.width * c->own_rows * sizeof(float4);
+  float* dst[3] = {pixels, normals, depth};
+  for (int k = 0; k < 3; ++k) {
+    if (!dst[k]) continue;
+    RT_HIP(c, rt::launch_gbuf_convert(xfer_desc(c, k, 1), c->stream));
+    RT_HIP(c, hipMemcpyAsync(dst[k], c->d_xfer, bytes, hipMemcpyDeviceToHost, c->stream));
   }
   if (image)
-    RT_HIP(c, hipMemcpy(image, c->d_image, (size_t)c->own_rows * c->cfg.width * 16, hipMemcpyDeviceToHost));
+    RT_HIP(c, hipMemcpyAsync(image, c->d_image, (size_t)c->own_rows * c->cfg.width * 16, hipMemcpyDeviceToHost,
+                             c->stream));
+  RT_HIP(c, hipStreamSynchronize(c->stream));
   return RT_OK;
 }
 
@@ -1121,26 +1096,18 @@ int rt_download_rect(rt_ctx* c, int x0, int x1, int y0, int y1, float* pixels, f
 int rt_upload_gbuffer(rt_ctx* c, const float* pixels, const float* normals, const float* depth) {
   if (!c) return RT_E_INVAL;
   RT_HIP(c, hipSetDevice(c->device));
-  const int F = c->cfg.num_frames;
-  const size_t slot = slot_elems(c);
-  const size_t ref_slot = (size_t)c->cfg.width * c->own_rows * 4;
-  std::vector<float> tmp(slot * 4), tmp2(slot * 4);
   int rc = join(c);
   if (rc == RT_OK) rc = sync_all(c);
+  if (rc == RT_OK && (pixels || normals || depth)) rc = xfer_buffer(c);
   if (rc != RT_OK) return rc;
-  for (int f = 0; f < F; ++f) {
-    struct { const float* src; float4* dst; } items[3] = {
-        {pixels, c->pix[c->pix_slot[f]]}, {normals, c->nrm[c->nrm_slot[f]]}, {depth, c->dep[c->dep_slot[f]]}};
-    for (int k = 0; k < 3; ++k) {
-      auto& it = items[k];
-      if (!it.src) continue;
-      RT_HIP(c, hipMemcpy(tmp2.data(), it.dst, slot * 16, hipMemcpyDeviceToHost));  // keep halo rows
-      planes_to_vec4(k, tmp2.data(), slot, tmp.data());
-      ref_to_dev(c, it.src + f * ref_slot, tmp.data());
-      vec4_to_planes(k, tmp.data(), slot, tmp2.data());
-      RT_HIP(c, hipMemcpy(it.dst, tmp2.data(), slot * 16, hipMemcpyHostToDevice));
-    }
+  const size_t bytes = (size_t)c->cfg.num_frames * c->cfg.width * c->own_rows * sizeof(float4);
+  const float* src[3] = {pixels, normals, depth};
+  for (int k = 0; k < 3; ++k) {  // (the halo rows of a strip keep their contents)
+    if (!src[k]) continue;
+    RT_HIP(c, hipMemcpyAsync(c->d_xfer, src[k], bytes, hipMemcpyHostToDevice, c->stream));
+    RT_HIP(c, rt::launch_gbuf_convert(xfer_desc(c, k, 0), c->stream));
   }
+  RT_HIP(c, hipStreamSynchronize(c->stream));
   return RT_OK;
 }
 

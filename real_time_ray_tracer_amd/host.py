@@ -247,6 +247,11 @@ class Renderer:
         return self._c(self._lib.rt_compute_frames(self.ctx, header._p(), mode, frame, n, rand_seed,
                                                    int(bool(light_movement))), "rt_compute_frames")
 
+    def set_frame_batch(self, max_frames: int):
+        """compute_frames' most frames per launch (modes 2-4); 1 = one launch and one image write
+        per frame, the reference's dispatch shape (rt_set_frame_batch)."""
+        self._c(self._lib.rt_set_frame_batch(self.ctx, int(max_frames)), "rt_set_frame_batch")
+
     def download(self, pixels=True, normals=True, depth=True, image=True) -> GBuffer:
         shp = (self.F, self.W, self.R, 4)
         p = np.empty(shp, np.float32) if pixels else None

@@ -108,8 +108,10 @@ def test_compute_frames_equals_frame_by_frame(mode, chunks):
     h = make_header("syn16p" if mode == 4 else "syn16", W, H, spp)
     n = sum(chunks) + 1
     outs = []
-    for many in (False, True):
+    for many in (False, True, "one launch per frame"):
         r = Renderer(W, H, h.S, h.AA)
+        if many == "one launch per frame":
+            r.set_frame_batch(1)  # rt_set_frame_batch: the reference's dispatch shape, same frames
         hh = h.copy()
         drv = FrameDriver(r, hh, mode, light_movement=True)
         if many:
@@ -121,11 +123,12 @@ def test_compute_frames_equals_frame_by_frame(mode, chunks):
                 drv.compute()
         outs.append((r.download(), hh.data.copy(), drv.frame_num))
         r.close()
-    (g0, h0, f0), (g1, h1, f1) = outs
-    assert f0 == f1 == n % 8
-    assert_bitwise(h1, h0, f"mode {mode} header")
-    for name in ("image", "pixels", "normals", "depth"):
-        assert_bitwise(getattr(g1, name), getattr(g0, name), f"mode {mode} {name}")
+    (g0, h0, f0) = outs[0]
+    for g1, h1, f1 in outs[1:]:
+        assert f0 == f1 == n % 8
+        assert_bitwise(h1, h0, f"mode {mode} header")
+        for name in ("image", "pixels", "normals", "depth"):
+            assert_bitwise(getattr(g1, name), getattr(g0, name), f"mode {mode} {name}")
 
 
 @pytest.mark.parametrize("scene", ["syn16", "syn16p"])
