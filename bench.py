@@ -581,7 +581,8 @@ def main():
         band_px = (r1 - r0 + (2 if mode in (1, 2) and world > 1 else 0)) * W
         hbm_alg = BYTES_PER_PIXEL[dom] * band_px / (avg_ms * 1e-3) / 1e9
         binfo = build_info()
-        traffic_data, traffic_src = load_traffic(args.config, binfo.get("src_sha1"))
+        # the committed PMC / SQ files are whole-frame launches: attached only at N = 1
+        traffic_data, traffic_src = load_traffic(args.config, binfo.get("src_sha1")) if world == 1 else (None, None)
         roof = {
             "bound": "valu",
             "achieved": round(tflops, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
@@ -611,7 +612,7 @@ def main():
         # per launch (SQ_INSTS_VALU, committed counter run) over what the launch could issue at
         # the spec rate (1 wave64 FP32 FMA per 2 clocks per SIMD, the peak above) and at the rate
         # a dense v_fma_f32 stream sustains on this GPU
-        sq, sq_src = load_sq(args.config, binfo.get("src_sha1"))
+        sq, sq_src = load_sq(args.config, binfo.get("src_sha1")) if world == 1 else (None, None)
         if sq:
             kern = next(iter(sq["kernels"].values()))
             insts = kern.get("SQ_INSTS_VALU")
