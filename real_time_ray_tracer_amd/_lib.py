@@ -139,7 +139,11 @@ def load() -> C.CDLL:
         except ImportError:
             pass
     lib = C.CDLL(str(path))
+    # RTRT_LIB (A/B tools) may name an older build: entry points added since are left unbound
+    tolerant = "RTRT_LIB" in os.environ
     for name, (res, args) in SIGNATURES.items():
+        if tolerant and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

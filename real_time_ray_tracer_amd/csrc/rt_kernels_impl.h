@@ -162,7 +162,15 @@ __device__ __forceinline__ float2 dep_load_xy(const float4* base, size_t off) { 
 // the history normals' xyz (aop_postprocessing.glsl:180), 12 B per history slot instead of 16;
 // the pixel itself and its neighbours read both planes.  rt_download / rt_upload_gbuffer convert
 // to the reference's vec4 layout.
+// (RT_NRM_PLANES=0: interleaved float4, the round-2 layout, for A/B builds)
+#ifndef RT_NRM_PLANES
+#define RT_NRM_PLANES 1
+#endif
 __device__ __forceinline__ void nrm_store(float4* base, size_t n, size_t off, float4 v) {
+  if (!RT_NRM_PLANES) {
+    base[off] = v;
+    return;
+  }
   float* p = (float*)base;
   p[3 * off] = v.x;
   p[3 * off + 1] = v.y;
@@ -170,10 +178,12 @@ __device__ __forceinline__ void nrm_store(float4* base, size_t n, size_t off, fl
   p[3 * n + off] = v.w;
 }
 __device__ __forceinline__ f3 nrm_load_xyz(const float4* base, size_t off) {
+  if (!RT_NRM_PLANES) return xyz(base[off]);
   const float* p = (const float*)base;
   return mk(p[3 * off], p[3 * off + 1], p[3 * off + 2]);
 }
 __device__ __forceinline__ float nrm_load_w(const float4* base, size_t n, size_t off) {
+  if (!RT_NRM_PLANES) return base[off].w;
   return ((const float*)base)[3 * n + off];
 }
 __device__ __forceinline__ float4 nrm_load(const float4* base, size_t n, size_t off) {
@@ -372,6 +382,9 @@ __device__ __forceinline__ bool bounce_cone_keep_pt(const ConeB& c, float4 g, fl
 //      1e-2 (|p - c_i| + r_i), so both roots are negative by more than 10x the computed-root error
 //      (bounce_cone_misses (1)): never above the 1e-4 threshold.
 // NaN anywhere fails both tests and keeps the cluster.
+#ifndef RT_TL_CLUSTERS
+#define RT_TL_CLUSTERS 1
+#endif
 #ifndef RT_GLOBAL_TAIL
 #define RT_GLOBAL_TAIL 1  // config (e), 256 spheres: 140.6 -> 128.3 ms per frame (r03i)
 #endif
@@ -904,8 +917,10 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
 // segment (plane_candidate) and, for the primary rays, culled against the pool cone.
 // MF: frame blockIdx.y of a multi-frame mode-2 launch (FrameParams::mf_rb): its own rand_buffer
 // and slot buffers, the image by the launch's last frame only.
+// CL: the bounce-ray cluster cull of the later bounce rounds (P.ncl > 0); without it the rounds
+// test every sphere.
 template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
-          int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false>
+          int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false, bool CL = true>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   // CNT = false: the work counters compiled out (timed launches pass none): fewer live scalars
   unsigned long long* const cnts = CNT ? P.counters : nullptr;
@@ -940,7 +955,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   float4* geol = (float4*)(lbase + LO.geol);  // [nobj] when TAIL && nobj <= kTailMaxObj
   // split tail rounds: the sphere table in LDS up to kTailMaxObj spheres; above (TAIL instantiations
   // launched without the LDS table), per-lane reads of the global table (L1/L2-resident)
-  const bool tail_lds = TAIL && nobj <= kTailMaxObj;
+  constexpr bool tail_lds = TAIL && PT;  // launch_batch: the LDS-table instantiations (<= kTailMaxObj) have PT
   const bool tail_ok = TAIL;
   const float4* const tgeo = tail_lds ? geol : geo;
   // PT: the batched first bounce keeps its per-ray pre-test table in the same LDS rows, so the
@@ -1349,7 +1364,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       const f3 d = mk(__shfl(dir.x, owner), __shfl(dir.y, owner), __shfl(dir.z, owner));
       float t = -1.0f;
       int ind = -1;
-      if (P.ncl > 0 && G <= kClusterTailMaxG) {
+      if (CL && P.ncl > 0 && G <= kClusterTailMaxG) {
         // cluster cull over the round's L paths (cluster_may_hit): lane pl of group g tests
         // clusters pl, pl + G, ... for path g; the ballot folded over the groups gives the clusters
         // some path may hit.  Their spheres plus the always-tested ones, compacted in ascending
@@ -1394,7 +1409,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       }
       float tt = __shfl(t, rk * G);
       int ii = __shfl(ind, rk * G);
-      if (!(P.ncl > 0 && G <= kClusterTailMaxG)) exec_tests += (unsigned long long)((nobj + G - 1) / G);
+      if (!(CL && P.ncl > 0 && G <= kClusterTailMaxG)) exec_tests += (unsigned long long)((nobj + G - 1) / G);
       if (has) {
         if (PL) plane_pass(P, pos, dir, 0.0001f, tt, ii);
         ++nseg;
@@ -1406,7 +1421,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       continue;
     }
     // ---- one bounce segment for every live path, against every sphere ------------------
-    exec_tests += (unsigned long long)(P.ncl > 0 ? P.ncl : nobj);
+    exec_tests += (unsigned long long)(CL && P.ncl > 0 ? P.ncl : nobj);
     if (ABL == 7) {  // later bounce rounds: sphere iterations, and those with any live lane's del >= 0
       tsec[6] += (unsigned long long)nobj;
       for (int i = 0; i < nobj; ++i) {
@@ -1417,7 +1432,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         tsec[7] += __ballot(has && del >= 0.0f) != 0;
       }
     }
-    if (P.ncl > 0) {
+    if (CL && P.ncl > 0) {
       // cluster cull: a cluster is skipped when no live lane's ray may hit it (cluster_may_hit);
       // the spheres of the kept clusters plus the always-tested ones are visited in ascending
       // index order, so (t, ind) is the full scan's (ao_compute.glsl:183-194)
@@ -1727,18 +1742,19 @@ size_t tab_lds_bytes(const FrameParams& p) { return (size_t)5 * (p.nobj > 0 ? p.
 template <int SPPC, bool PL>
 inline void launch_batch(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStream_t stream, const FrameParams& q) {
   constexpr bool GT = RT_GLOBAL_TAIL;  // split tail rounds above kTailMaxObj spheres (global table)
+  constexpr bool TLC = RT_TL_CLUSTERS;  // the cluster cull in the LDS-table (<= kTailMaxObj) instantiations
   if (q.mf_n > 0) {  // multi-frame mode-2 launch (never with counters: rt_compute_frames checks)
     g.y = (unsigned)q.mf_n;
     if (tl)
-      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL, true>), g, b, lds, stream, q, q.sph);
+      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL, true, TLC>), g, b, lds, stream, q, q.sph);
     else
       hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, false, PL, true>), g, b, lds, stream, q, q.sph);
     return;
   }
   if (tl && cnt)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, true, PL>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, true, PL, false, TLC>), g, b, lds, stream, q, q.sph);
   else if (tl)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL, false, TLC>), g, b, lds, stream, q, q.sph);
   else if (cnt)
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, true, PL>), g, b, lds, stream, q, q.sph);
   else

@@ -1080,7 +1080,11 @@ int rt_download_rect(rt_ctx* c, int x0, int x1, int y0, int y1, float* pixels, f
     for (int k = 0; k < 3; ++k) {
       auto& it = items[k];
       if (!it.dst) continue;
-      RT_HIP(c, k == kPixels ? rect(it.src, y0 - c->band0) : split_rect(it.src, y0 - c->band0, k == kNormals ? 3 : 2));
+#ifndef RT_NRM_PLANES
+#define RT_NRM_PLANES 1
+#endif
+      RT_HIP(c, (k == kPixels || (k == kNormals && !RT_NRM_PLANES)) ? rect(it.src, y0 - c->band0)
+                                                                   : split_rect(it.src, y0 - c->band0, k == kNormals ? 3 : 2));
       float* out = it.dst + (size_t)f * w * h * 4;  // [w][h] vec4, y fastest (reference layout)
       for (int x = 0; x < w; ++x)
         for (int r = 0; r < h; ++r) std::memcpy(out + ((size_t)x * h + r) * 4, &tmp[(size_t)r * w + x], 16);
