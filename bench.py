@@ -600,6 +600,10 @@ def main():
             "tests_per_launch": tests,
             "segments_per_sample": round(counts["segments"] / max(counts["samples"], 1), 4),
             "useful_test_ratio": round(counts["tests"] / max(counts["executed_lane_tests"], 1), 4),
+            "basis": ("algorithmic: the reference's brute-force ray-shape tests (every segment tests every shape, "
+                      "20 FLOP each) per kernel second; the kernels skip provably missed tests (culling), so this "
+                      "can exceed the hardware peak when useful_test_ratio is high; valu_issue (when present) is "
+                      "the hardware's own view"),
             "hbm": {"achieved": round(hbm_alg, 2), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                     "frac": round(hbm_alg / PEAK_HBM_GBPS, 6),
                     "bytes_per_launch": BYTES_PER_PIXEL[dom] * band_px},
