@@ -24,4 +24,4 @@ tail -3 $O/strip_scaling_n8_calibrated.txt
 timeout -k 10 600 python -u tools/strip_scaling.py --config e --n 8 --frames 4 --calibrate --warm-ms 300 > $O/strip_scaling_e_n8_calibrated.txt 2>&1 || exit 1
 tail -3 $O/strip_scaling_e_n8_calibrated.txt
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29537 bench.py --gpus 4 --backend gloo --steps 6 --warmup 8 --no-cpu-baseline > $O/gloo_n4.json 2> $O/gloo_n4.err || { tail -20 $O/gloo_n4.err; exit 1; }
-python3 -c "import json; d=json.load(open('$O/gloo_n4.json')); print(d['value'], d['verify'], d['collective'], d['config']['strips'])"
+python3 -c "import json; d=json.loads([l for l in open('$O/gloo_n4.json') if l.startswith('{')][-1]); print(d['value'], d['verify'], d['collective'], d['config']['strips'])"
