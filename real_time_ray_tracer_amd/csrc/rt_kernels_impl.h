@@ -1555,16 +1555,6 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
 __device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, unsigned& filtered, unsigned& visited,
                                            unsigned& accepted);
 
-__device__ __forceinline__ float nbr_weight(f3 n, float nd, float nb, const float4* nrm, size_t np, const float4* dep,
-                                            size_t o) {
-  if (nrm_load_w(nrm, np, o) < 0.001f) return 1.0f;  // (its normal xyz and depth are not read)
-  const float2 kd = dep_load_xy(dep, o);
-  float normal_dot = dot(n, nrm_load_xyz(nrm, o));
-  float depth_diff = 1.0f - gclamp(fabsf(nd - kd.x), 0.0f, 1.0f);
-  float bounces_diff = 1.0f - gclamp(fabsf(nb - kd.y) / 1.7f, 0.0f, 1.0f);
-  return normal_dot * depth_diff * bounces_diff + 0.2f;
-}
-
 // XCD-local tile order: workgroups are dealt round-robin to the 8 XCDs (linear block id L on
 // XCD L mod 8), each with its own L2, so in plain row-major order horizontally adjacent tiles
 // sit on different XCDs and every tile's left / right neighbour columns (whole 128-B lines of
@@ -1609,56 +1599,117 @@ __global__ __launch_bounds__(kBlock) void post_kernel(FrameParams P) {
   }
 }
 
+// History slots read ahead of the acceptance test (see post_pixel).  1: the next slot's keys and
+// colour are in flight while a slot is tested.  2 needs 76 VGPRs, more than the 72 an AO wave
+// holds, so a post-process wave no longer fits in the registers one retiring AO wave frees and
+// pipelined frames got 8% slower (profiles/r03s_ab_post_prefetch.txt).
+constexpr int kPostAhead = 1;
+struct HistSlot {
+  f3 n;
+  float2 d;
+  float4 p;
+};
+__device__ __forceinline__ HistSlot hist_load(const FrameParams& P, int cf, size_t off) {
+  HistSlot h;
+  h.n = nrm_load_xyz(P.hist_nrm[cf], off);
+  h.d = dep_load_xy(P.hist_dep[cf], off);
+  h.p = P.hist_pix[cf][off];
+  return h;
+}
+
 __device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, unsigned& filtered, unsigned& visited,
                                            unsigned& accepted) {
-  const int W = P.W, f = P.frame;
+  const int W = P.W, f = P.frame, F = P.F;
   const size_t off = (size_t)(y - P.band_row0) * W + x;
   float4 color = P.raw[off];
   const size_t np = dep_plane(P);  // normals: xyz plane + w plane (nrm_store)
   if (nrm_load_w(P.nrm, np, off) > 0.99f) {
     filtered = 1;
+    // Memory round trips, not bytes, are what this kernel costs in the pipelined frame: there it
+    // runs beside the next frame's AO pass, and each resident post-process wave holds registers
+    // an AO wave could use for as long as it waits on memory.  So the neighbours are requested in
+    // one round trip, and history slots f-1, f-2, ... kPostAhead ahead of the acceptance test with
+    // keys and colour together (the colour of the slot that fails is read and dropped): ~F + 2
+    // round trips per filtered pixel instead of ~2F + 9 (pipelined frames 2.368 -> 2.305 ms,
+    // profiles/r03u_ab_post_round_trips.txt).  The arithmetic is the reference's, in its order.
     const float2 cd = dep_load_xy(P.dep, off);
     const f3 nv = nrm_load_xyz(P.nrm, off);
     const float nd = cd.x, nb = cd.y;
     float4 acc = color;
     float den = 1.0f;
     const int band_end = P.band_row0 + P.band_rows;
-    // GLSL order: up, down, left, right (line 173)
+    // GLSL order: up, down, left, right (line 173).  Every neighbour's flag, keys and colour are
+    // requested together (an absent neighbour reads the pixel itself and is dropped).
+    {
+      size_t o[4];
+      bool pr[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      int xx = x + (k == 2 ? -1 : (k == 3 ? 1 : 0));
-      int yy = y + (k == 0 ? 1 : (k == 1 ? -1 : 0));
-      bool present = (k == 0) ? (y + 1 < P.H) : (k == 1) ? (y >= 2) : (k == 2) ? (x > 0) : (x + 1 < W);
-      present = present && yy >= P.band_row0 && yy < band_end;
-      float wk = 0.0f;
-      float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      if (present) {
-        size_t o = (size_t)(yy - P.band_row0) * W + xx;
-        wk = nbr_weight(nv, nd, nb, P.nrm, np, P.dep, o);
-        v = P.raw[o];
+      for (int k = 0; k < 4; ++k) {
+        int xx = x + (k == 2 ? -1 : (k == 3 ? 1 : 0));
+        int yy = y + (k == 0 ? 1 : (k == 1 ? -1 : 0));
+        bool present = (k == 0) ? (y + 1 < P.H) : (k == 1) ? (y >= 2) : (k == 2) ? (x > 0) : (x + 1 < W);
+        pr[k] = present && yy >= P.band_row0 && yy < band_end;
+        const int xc = pr[k] ? xx : x, yc = pr[k] ? yy : y;  // (a select, not a branch on a shared load)
+        o[k] = (size_t)(unsigned)((yc - P.band_row0) * W + xc);
       }
-      acc.x = acc.x + wk * v.x; acc.y = acc.y + wk * v.y;
-      acc.z = acc.z + wk * v.z; acc.w = acc.w + wk * v.w;
-      den = den + wk;
+      float wn[4];
+      f3 nn[4];
+      float2 dd[4];
+      float4 rv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        wn[k] = nrm_load_w(P.nrm, np, o[k]);
+        nn[k] = nrm_load_xyz(P.nrm, o[k]);
+        dd[k] = dep_load_xy(P.dep, o[k]);
+        rv[k] = P.raw[o[k]];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        // the neighbour weight (aop_postprocessing.glsl:82-171: 1 for a sky neighbour), branch-free
+        // so the compiler keeps the loads above together
+        const float normal_dot = dot(nv, nn[k]);
+        const float depth_diff = 1.0f - gclamp(fabsf(nd - dd[k].x), 0.0f, 1.0f);
+        const float bounces_diff = 1.0f - gclamp(fabsf(nb - dd[k].y) / 1.7f, 0.0f, 1.0f);
+        const float wf = normal_dot * depth_diff * bounces_diff + 0.2f;
+        const float wk = pr[k] ? (wn[k] < 0.001f ? 1.0f : wf) : 0.0f;
+        const float4 v = pr[k] ? rv[k] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        acc.x = acc.x + wk * v.x; acc.y = acc.y + wk * v.y;
+        acc.z = acc.z + wk * v.z; acc.w = acc.w + wk * v.w;
+        den = den + wk;
+      }
     }
     color = make_float4(acc.x / den, acc.y / den, acc.z / den, acc.w / den);
     // temporal, lines 177-201
+    HistSlot ring[kPostAhead];
+    int cf = f;
+    int issued = 0;
+#pragma unroll
+    for (int k = 0; k < kPostAhead; ++k)
+      if (k < F - 1) {
+        cf = cf == 0 ? F - 1 : cf - 1;
+        ring[k] = hist_load(P, cf, off);
+        ++issued;
+      }
     float4 cs = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     float denominator = 0.9f;
-    for (int i = 1; i < P.F; ++i) {
-      int cf = (f + P.F - i) % P.F;
-      const f3 hn = nrm_load_xyz(P.hist_nrm[cf], off);
-      const float2 hd = dep_load_xy(P.hist_dep[cf], off);
-      float normal_dot = dot(nv, hn);
-      float depth_diff = 1.0f - gclamp(fabsf(nd - hd.x), 0.0f, 1.0f);
-      float bounces_diff = 1.0f - gclamp(fabsf(nb - hd.y) / 1.7f, 0.0f, 1.0f);
+    for (int i = 1; i < F; ++i) {
+      const HistSlot h = ring[0];
+#pragma unroll
+      for (int k = 0; k + 1 < kPostAhead; ++k) ring[k] = ring[k + 1];
+      if (issued < F - 1) {  // slot f-i-kPostAhead, in flight while slot f-i is tested
+        cf = cf == 0 ? F - 1 : cf - 1;
+        ring[kPostAhead - 1] = hist_load(P, cf, off);
+        ++issued;
+      }
+      float normal_dot = dot(nv, h.n);
+      float depth_diff = 1.0f - gclamp(fabsf(nd - h.d.x), 0.0f, 1.0f);
+      float bounces_diff = 1.0f - gclamp(fabsf(nb - h.d.y) / 1.7f, 0.0f, 1.0f);
       float coeff = normal_dot * depth_diff * bounces_diff;
       ++visited;
       if (!(coeff > 0.85f)) break;
       ++accepted;
-      float4 hp = P.hist_pix[cf][off];
-      cs.x = cs.x + coeff * hp.x; cs.y = cs.y + coeff * hp.y;
-      cs.z = cs.z + coeff * hp.z; cs.w = cs.w + coeff * hp.w;
+      cs.x = cs.x + coeff * h.p.x; cs.y = cs.y + coeff * h.p.y;
+      cs.z = cs.z + coeff * h.p.z; cs.w = cs.w + coeff * h.p.w;
       denominator = denominator + coeff;
     }
     color = make_float4((color.x * 0.9f + cs.x) / denominator, (color.y * 0.9f + cs.y) / denominator,

@@ -220,6 +220,7 @@ static bool ab_general() {
 
 hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream) {
   if (p.trace_rows <= 0) return hipSuccess;
+  if (const char* es = getenv("RTRT_POST_SKIP"); es && atoi(es) == 1 && program == K_POST) return hipSuccess;  // A/B floor
   FrameParams q = launch_params(p);
   const bool pl = p.nplanes > 0;
   if (program == K_AOP || program == K_AO) {
