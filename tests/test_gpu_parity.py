@@ -373,3 +373,40 @@ def test_errors_are_reported():
     r.close()
     with pytest.raises(_lib.RtError):
         Renderer(16, 16, 4, 300)  # spp above the supported 256
+
+
+@pytest.mark.parametrize("mode,pipelined", [(1, False), (1, True), (2, False), (3, False), (4, False)])
+@pytest.mark.parametrize("W,H", [(1, 1), (1, 6), (9, 1), (2, 3), (17, 5)])
+def test_degenerate_frame_sizes(W, H, mode, pipelined):
+    """Frames of one row / one column / a few pixels: partial pools and tiles everywhere, and
+    every post-process neighbour test (aop_postprocessing.glsl:82-171) at its border value,
+    over 10 frames so the 8-slot history ring wraps (the post-process reads every slot)."""
+    spp = 4
+    h0 = make_header("s1", W, H, spp)
+    r = Renderer(W, H, h0.S, spp)
+    if pipelined:
+        r.enable_pipelining(True)
+    hg, ho = h0.copy(), h0.copy()
+    s = SSBO(ho, W, H)
+    d = oracle.dims(W, H, h0.S, spp)
+    img = np.zeros((H, W, 4), np.float32)
+    fg = fo = 0
+    for k in range(10 if mode in (1, 2) else 3):
+        for hh, f in ((hg, fg), (ho, fo)):
+            if mode in (1, 2):
+                hh.fill_rand_buffer(7000 + k)
+            else:
+                hh.moving_light(True)
+            hh.set_mode(f, hh.num_objects)
+        r.upload_header(hg)
+        fg = r.dispatch(mode, fg)
+        s.set_header(ho)
+        fo = oracle.dispatch(s.data, d, mode, fo, img)
+        assert fg == fo
+    g = r.download()
+    r.close()
+    what = f"{W}x{H} mode {mode}{' pipelined' if pipelined else ''}"
+    assert_close(g.image, img, f"{what} image")
+    assert_close(g.pixels, s.pixels, f"{what} pixels")
+    assert_bitwise(g.normals, s.normals, f"{what} normals")
+    assert_bitwise(g.depth, s.depth, f"{what} depth")
