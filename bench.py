@@ -253,6 +253,10 @@ def main():
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 also renders every frame whole and checks the gathered frames bit for bit "
                          "(without it, N > 1 still checks the first 2 gathered frames, before the timed region)")
+    ap.add_argument("--frame-batch", type=int, default=0,
+                    help="modes 2-4: most frames per launch in the C++ frame loop (rt_set_frame_batch); 0 = the "
+                         "library's default (multi-frame launches); 1 = one launch per frame, the form the "
+                         "committed per-frame PMC / SQ counter runs use (tools/pmc_config.sh BENCH_ARGS)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N>1 path with ranks sharing GPUs, gather staged through host")
     args = ap.parse_args()
@@ -365,6 +369,8 @@ def main():
     plan = StripPlan(W, H, bounds)
     r0, r1 = plan.rows(rank)
     rend = Renderer(W, H, S, spp, device=gpu, rows=(r0, r1))
+    if args.frame_batch > 0:
+        rend.set_frame_batch(args.frame_batch)
     rend.set_stream(stream)
     # pipelined mode 1: post-process (and the image consumers: the gather) on a second stream
     pipeline = mode == 1 and not args.no_pipeline
@@ -518,7 +524,7 @@ def main():
         state["frame"] = rend.compute_frames(header, mode, state["frame"], args.steps, 7000 + warm, False)
         torch.cuda.synchronize()
         pf_s = (time.perf_counter() - t0p) / args.steps
-        rend.set_frame_batch(32)
+        rend.set_frame_batch(args.frame_batch if args.frame_batch > 0 else 32)
         per_frame = {"ms_per_step": round(pf_s * 1e3, 4),
                      "value": round(W * H * (spp if mode in (1, 2) else 1) / pf_s / 1e6, 2),
                      "dispatch": "one launch and one image write per frame (rt_set_frame_batch(1)), C++ frame loop, "
@@ -585,6 +591,14 @@ def main():
         binfo = build_info()
         # the committed PMC / SQ files are whole-frame launches: attached only at N = 1
         traffic_data, traffic_src = load_traffic(args.config, binfo.get("src_sha1")) if world == 1 else (None, None)
+        # a counter run's values are per dispatch: with multi-frame launches (modes 2-4 in the C++
+        # loop) a dispatch holds up to F frames, so only runs taken one frame per dispatch
+        # (--frame-batch 1, recorded as frames_per_dispatch) are comparable with a per-frame kernel_ms
+        per_dispatch_ok = lambda d: d is not None and (not host_loop or d.get("frames_per_dispatch") == 1)
+        hw_note = None
+        if traffic_data is not None and not per_dispatch_ok(traffic_data):
+            hw_note = f"{traffic_src}: per multi-frame dispatch, not per frame; omitted"
+            traffic_data, traffic_src = None, None
         roof = {
             "bound": "valu",
             "achieved": round(tflops, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
@@ -619,8 +633,18 @@ def main():
         # the spec rate (1 wave64 FP32 FMA per 2 clocks per SIMD, the peak above) and at the rate
         # a dense v_fma_f32 stream sustains on this GPU
         sq, sq_src = load_sq(args.config, binfo.get("src_sha1")) if world == 1 else (None, None)
+        if sq is not None and not per_dispatch_ok(sq):
+            hw_note = (hw_note + "; " if hw_note else "") + f"{sq_src}: per multi-frame dispatch, not per frame; omitted"
+            sq, sq_src = None, None
+        if hw_note:
+            roof["hardware_counters_note"] = hw_note
         if sq:
-            kern = next(iter(sq["kernels"].values()))
+            # the dominant program's kernel; of its instantiations the one with the most dispatches
+            # (the timed form, not the counted one) where the file records dispatch counts
+            sub = {1: "ao_", 3: "ao_", 4: "phong", 5: "hybrid"}[dom]
+            names = [k for k in sq["kernels"] if sub in k] or list(sq["kernels"])
+            disp = sq.get("dispatches", {})
+            kern = sq["kernels"][max(names, key=lambda k: disp.get(k, 0))]
             insts = kern.get("SQ_INSTS_VALU")
             if insts:
                 spec = PEAK_FP32_TFLOPS * 1e12 / 128 * avg_ms * 1e-3

@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
 # SQ counter passes for one bench config (one rocprofv3 --pmc run per counter group, no
 # tracing domains), summarised per kernel: tools/pmc_config.sh <tag> <config> [kernel-substring]
+# BENCH_ARGS: extra bench.py arguments (modes 2-4: "--frame-batch 1" for per-frame counters)
 set -euo pipefail
 TAG=$1
 CFG=$2
@@ -19,7 +20,7 @@ for G in "$G1" "$G2" $([ -n "$G3" ] && echo "G3"); do
   [ "$G" = "G3" ] && G="$G3"
   i=$((i+1))
   timeout -k 10 120 rocprofv3 --pmc $G --output-format csv -d "$OUT/${CFG}_g$i" -o run -- \
-    python3 bench.py --config "$CFG" --steps 10 --warmup 8 --no-cpu-baseline > "$OUT/${CFG}_g$i.log" 2>&1
+    python3 bench.py --config "$CFG" --steps 10 --warmup 8 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/${CFG}_g$i.log" 2>&1
 done
 python3 - "$OUT" "$CFG" "$KSUB" <<'EOF'
 import csv, glob, os, sys, collections
@@ -40,10 +41,14 @@ try:  # the library build the counters were taken on (make lib writes BUILD_INFO
 except Exception:
     info = {}
 out_json = {"config": cfg, "kernels": {}, "src_sha1": info.get("src_sha1"), "commit": info.get("commit"),
-            "units": "per dispatch, mean over the dispatches of the bench run (warm-up, timed, standalone, counted)"}
+            "units": "per dispatch, mean over the dispatches of the bench run (warm-up, timed, standalone, counted)",
+            "bench_args": os.environ.get("BENCH_ARGS", ""),
+            # one frame per dispatch: mode 1 always; modes 2-4 only with --frame-batch 1
+            "frames_per_dispatch": 1 if cfg in ("d", "p", "q", "s1") or "--frame-batch 1" in os.environ.get("BENCH_ARGS", "") else None}
 for k, cs in res.items():
     avg = {c: round(sum(v) / len(v)) for c, v in sorted(cs.items())}
     print(cfg, k, avg, "dispatches", max(len(v) for v in cs.values()))
     out_json["kernels"][k] = avg
+    out_json.setdefault("dispatches", {})[k] = max(len(v) for v in cs.values())
 json.dump(out_json, open(os.path.join(out, f"sq_{cfg}.json"), "w"), indent=1)
 EOF

@@ -45,7 +45,10 @@ def main():
     mode_cfg = {"a": 3, "b": 4, "c": 2, "d": 1, "e": 2, "p": 1, "q": 1, "s1": 1}[cfg]
     fe = collect(fetch_dir, "FETCH_SIZE", mode_cfg)
     wr = collect(write_dir, "WRITE_SIZE", mode_cfg)
-    res = {"config": cfg, "units": "bytes per launch (FETCH_SIZE*2*1024 + WRITE_SIZE*1024, median)"}
+    res = {"config": cfg, "units": "bytes per launch (FETCH_SIZE*2*1024 + WRITE_SIZE*1024, median)",
+           "bench_args": os.environ.get("BENCH_ARGS", ""),
+           # one frame per dispatch: mode 1 always; modes 2-4 only with --frame-batch 1
+           "frames_per_dispatch": 1 if mode_cfg == 1 or "--frame-batch 1" in os.environ.get("BENCH_ARGS", "") else None}
     try:  # the library build the counters were taken on (make lib writes BUILD_INFO)
         info = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
                                            "real_time_ray_tracer_amd", "BUILD_INFO")))

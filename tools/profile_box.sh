@@ -2,6 +2,7 @@
 # Run on the GPU box (via gpurun): bench + rocprofv3 kernel trace + separate PMC passes.
 #   tools/profile_box.sh <tag> [config] [steps]
 # Outputs under gpurun_out/<tag>/ (summaries to be copied into profiles/).
+# BENCH_ARGS: extra bench.py arguments for the PMC passes (modes 2-4: "--frame-batch 1").
 set -euo pipefail
 TAG=${1:-r01}
 CFG=${2:-d}
@@ -20,8 +21,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_seq" -o run -- \
   python3 bench.py --config "$CFG" --steps 10 --warmup 8 --no-cpu-baseline --no-pipeline > "$OUT/kt_seq_bench.json" 2> "$OUT/kt_seq.err"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-  python3 bench.py --config "$CFG" --steps 3 --warmup 8 --no-cpu-baseline > /dev/null 2> "$OUT/pmc_fetch.err"
+  python3 bench.py --config "$CFG" --steps 3 --warmup 8 --no-cpu-baseline ${BENCH_ARGS:-} > /dev/null 2> "$OUT/pmc_fetch.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-  python3 bench.py --config "$CFG" --steps 3 --warmup 8 --no-cpu-baseline > /dev/null 2> "$OUT/pmc_write.err"
+  python3 bench.py --config "$CFG" --steps 3 --warmup 8 --no-cpu-baseline ${BENCH_ARGS:-} > /dev/null 2> "$OUT/pmc_write.err"
 find "$OUT" -name "*.csv" | head -50
 python3 tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$CFG" "$OUT/pmc.json"
