@@ -1,0 +1,10 @@
+# r03z: re-check of the restored tree (GPU suite, smoke, the driver's bench command)
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r03z; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1 || { tail -30 $O/gpu_tests.txt; exit 1; }
+tail -2 $O/gpu_tests.txt
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { cat $O/smoke.txt; exit 1; }
+cat $O/smoke.txt
+timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
+cat $O/bench.json
