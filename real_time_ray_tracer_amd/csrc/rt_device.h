@@ -84,13 +84,19 @@ __device__ __forceinline__ float det_sin(float x) {
   r = fmaf(-k, -1.71512451e-15f, r);
   // quadrant q = k mod 4 from the integer k (v_cvt_i32_f32 saturates beyond 2^31; the oracle
   // mirrors that): bit 0 picks cos, bit 1 flips the sign, both read from k << 30
-  const unsigned qs = (unsigned)(int)k << 30;
+  const int ki = (int)k;
+  const unsigned qs = (unsigned)ki << 30;
   float z = r * r;
   float s = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
   float c = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
                  fmaf(-0.5f, z, 1.0f));
-  const float v = (qs & 0x40000000u) ? c : s;
-  return __uint_as_float(__float_as_uint(v) ^ (qs & 0x80000000u));
+  // cos for odd k: the select as a bit mask (bit 0 of k sign-extended, v_bfe_i32) and a bitwise
+  // merge (v_bfi_b32), instead of an and, a compare into VCC (with its wait states) and a
+  // cndmask.  Written out: the compiler turns the C form back into the compare and cndmask.
+  unsigned sel, v;
+  asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(sel) : "v"(ki));
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(v) : "v"(sel), "v"(__float_as_uint(c)), "v"(__float_as_uint(s)));
+  return __uint_as_float(v ^ (qs & 0x80000000u));
 }
 
 // IEEE binary32 square root, correctly rounded: the value sqrtf() has under

@@ -1184,7 +1184,12 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         return normalize(mk(a * 2.0f - 1.0f, b * 2.0f - 1.0f, e * 2.0f - 1.0f));
       };
       if (!LAZY) bhemi = hemisphere();
-      bpos = cam;
+      // the camera in VGPRs for the primary tests: with the uniform camera and the sphere both in
+      // SGPRs, each of the three subtractions would need a copy first (one scalar operand per
+      // vector instruction)
+      f3 cv = cam;
+      asm("" : "+v"(cv.x), "+v"(cv.y), "+v"(cv.z));
+      bpos = cv;
       br = bg = bb = 1.0f;
       float t = -1.0f;
       int ind = -1;
