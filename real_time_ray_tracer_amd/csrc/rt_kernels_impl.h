@@ -920,13 +920,16 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
 // CL: the bounce-ray cluster cull of the later bounce rounds (P.ncl > 0); without it the rounds
 // test every sphere.
 template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
-          int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false, bool CL = true>
+          int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false, bool CL = true, int DC = 0,
+          bool CLON = false>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   // CNT = false: the work counters compiled out (timed launches pass none): fewer live scalars
   unsigned long long* const cnts = CNT ? P.counters : nullptr;
   unsigned long long* const rowc = CNT ? P.row_counters : nullptr;
   extern __shared__ float4 lds[];
-  const int spp = SPPC ? SPPC : P.spp, W = P.W, D = P.D, nobj = P.nobj;
+  const int spp = SPPC ? SPPC : P.spp, W = P.W, D = DC ? DC : P.D, nobj = P.nobj;
+  // CLON: launched only with clusters (P.ncl > 0), so the rounds' plain full-scan path is not compiled
+  const bool use_cl = CL && (CLON || P.ncl > 0);
   // this frame's buffers (the launch's frame unless MF)
   const int fj = MF ? (int)blockIdx.y : 0;
   const int fslot = MF ? (P.mf_slot0 + fj) % P.F : 0;
@@ -966,8 +969,19 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     for (int k = lane; k < nobj; k += 64) geol[k] = geo[k];
     geol_valid = true;
   }
-  const float4* col = P.shapes + 2 * P.S;
-  const float4* aux = P.shapes + 3 * P.S;
+  // col[ind] / aux[ind] (rt_device.h scene tables) addressed from the sphere table (geo = shapes + 4S, launch_program) with a
+  // per-lane offset the compiler cannot fold into a hoisted pointer: the two extra 64-bit base
+  // pointers were the most reloaded of the kernel's scalar spills (a v_readlane pair each, per shade)
+  auto col_at = [&](int ind) -> float4 {
+    int o = ind - P.S;
+    asm("" : "+v"(o));
+    return geo[o - P.S];
+  };
+  auto aux_at = [&](int ind) -> float4 {
+    int o = ind - P.S;
+    asm("" : "+v"(o));
+    return geo[o];
+  };
 
   const long long npix = (long long)P.trace_rows * W;
   // pool of this workgroup
@@ -1115,8 +1129,16 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     int kind = PRIM_MISS;
     bool go = false;
     if (ind != -1) {
-      att = col[ind];
-      if (aux[ind].x > 0.9f) {
+      att = col_at(ind);
+      const float4 ax = aux_at(ind);
+      // all-sphere scenes: the hit sphere's centre requested with its colour and flags, one memory
+      // round trip (pinned here: the compiler would sink the load behind the emissive test)
+      float4 gc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (!PL) {
+        gc = geo[ind];
+        asm volatile("" ::"v"(gc.x), "v"(gc.y), "v"(gc.z));
+      }
+      if (ax.x > 0.9f) {
         kind = PRIM_EMISSIVE;
       } else {
         kind = PRIM_HIT;
@@ -1126,11 +1148,11 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           const float4 gi = P.shapes[ind];
           nn = __float_as_int(P.shapes[P.S + ind].w) == SHAPE_PLANE ? xyz(gi) : normalize(curr - xyz(gi));
         } else {
-          nn = normalize(curr - xyz(geo[ind]));
+          nn = normalize(curr - xyz(gc));
         }
         if (aa == 0 && first) prec[lp] = make_float4(nn.x, nn.y, nn.z, t);
         ps = curr;
-        const float reflect = aux[ind].y;
+        const float reflect = ax.y;
         f3 X;
         if (reflect > 0.999f) {
           X = hm + nn;
@@ -1174,8 +1196,8 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       }
       bdir = primary_dir(P, hp, vp);
       // get_pt_within_unit_sphere(aa), hoisted: it depends on aa and the pixel only, so it is
-      // computed once per sample — after the primary hit when LAZY (only a non-emissive hit
-      // uses it)
+      // computed once per sample — after the primary hit when LAZY, for hits only (a non-emissive
+      // hit uses it)
       auto hemisphere = [&]() {
         float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
         float a = grandom(f.x + px * s.z, f.y + py * s.w);
@@ -1212,7 +1234,9 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       }
       if (PL) plane_pass_masked(P, pmask, bpos, bdir, 0.0001f, t, ind);
       ++nseg;
-      if (LAZY && ind != -1 && !(aux[ind].x > 0.9f)) bhemi = hemisphere();
+      // (every hit, emissive or not: only non-emissive hits use it, but waiting for the hit's flags
+      // first cost a memory round trip, and a wave with any non-emissive hit computes it anyway)
+      if (LAZY && ind != -1) bhemi = hemisphere();
       live = shade(ind, t, bpos, bdir, bhemi, br, bg, bb, D, bitem, true);
     }
     bdepth = D - 1;
@@ -1369,7 +1393,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       const f3 d = mk(__shfl(dir.x, owner), __shfl(dir.y, owner), __shfl(dir.z, owner));
       float t = -1.0f;
       int ind = -1;
-      if (CL && P.ncl > 0 && G <= kClusterTailMaxG) {
+      if (use_cl && G <= kClusterTailMaxG) {
         // cluster cull over the round's L paths (cluster_may_hit): lane pl of group g tests
         // clusters pl, pl + G, ... for path g; the ballot folded over the groups gives the clusters
         // some path may hit.  Their spheres plus the always-tested ones, compacted in ascending
@@ -1414,7 +1438,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       }
       float tt = __shfl(t, rk * G);
       int ii = __shfl(ind, rk * G);
-      if (!(CL && P.ncl > 0 && G <= kClusterTailMaxG)) exec_tests += (unsigned long long)((nobj + G - 1) / G);
+      if (!(use_cl && G <= kClusterTailMaxG)) exec_tests += (unsigned long long)((nobj + G - 1) / G);
       if (has) {
         if (PL) plane_pass(P, pos, dir, 0.0001f, tt, ii);
         ++nseg;
@@ -1426,7 +1450,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       continue;
     }
     // ---- one bounce segment for every live path, against every sphere ------------------
-    exec_tests += (unsigned long long)(CL && P.ncl > 0 ? P.ncl : nobj);
+    exec_tests += (unsigned long long)(use_cl ? P.ncl : nobj);
     if (ABL == 7) {  // later bounce rounds: sphere iterations, and those with any live lane's del >= 0
       tsec[6] += (unsigned long long)nobj;
       for (int i = 0; i < nobj; ++i) {
@@ -1437,7 +1461,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         tsec[7] += __ballot(has && del >= 0.0f) != 0;
       }
     }
-    if (CL && P.ncl > 0) {
+    if (use_cl) {
       // cluster cull: a cluster is skipped when no live lane's ray may hit it (cluster_may_hit);
       // the spheres of the kept clusters plus the always-tested ones are visited in ascending
       // index order, so (t, ind) is the full scan's (ao_compute.glsl:183-194)
@@ -1795,26 +1819,28 @@ size_t tab_lds_bytes(const FrameParams& p) { return (size_t)5 * (p.nobj > 0 ? p.
 // The production pooled AO kernel: split tail rounds and the per-ray first-bounce pre-test when
 // the sphere table fits in LDS (tl), with or without the work counters (cnt), with or without
 // planes (PL).
-template <int SPPC, bool PL>
+constexpr int kRefDepth = 20;  // RECURSION_DEPTH, ao_compute.glsl:9
+
+template <int SPPC, bool PL, int DC = 0, bool CLON = false>
 inline void launch_batch(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStream_t stream, const FrameParams& q) {
   constexpr bool GT = RT_GLOBAL_TAIL;  // split tail rounds above kTailMaxObj spheres (global table)
   constexpr bool TLC = RT_TL_CLUSTERS;  // the cluster cull in the LDS-table (<= kTailMaxObj) instantiations
   if (q.mf_n > 0) {  // multi-frame mode-2 launch (never with counters: rt_compute_frames checks)
     g.y = (unsigned)q.mf_n;
     if (tl)
-      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL, true, TLC>), g, b, lds, stream, q, q.sph);
+      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL, true, TLC, DC, CLON>), g, b, lds, stream, q, q.sph);
     else
-      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, false, PL, true>), g, b, lds, stream, q, q.sph);
+      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, false, PL, true, true, DC, CLON>), g, b, lds, stream, q, q.sph);
     return;
   }
   if (tl && cnt)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, true, PL, false, TLC>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, true, PL, false, TLC, DC, CLON>), g, b, lds, stream, q, q.sph);
   else if (tl)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL, false, TLC>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL, false, TLC, DC, CLON>), g, b, lds, stream, q, q.sph);
   else if (cnt)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, true, PL>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, true, PL, false, true, DC, CLON>), g, b, lds, stream, q, q.sph);
   else
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, false, PL>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, false, PL, false, true, DC, CLON>), g, b, lds, stream, q, q.sph);
 }
 
 // g-buffer layout conversion (rt_download / rt_upload_gbuffer, the host-buffer path of
@@ -1886,8 +1912,15 @@ inline hipError_t launch_production(int program, const FrameParams& p, const Fra
     const bool cnt = p.counters || p.row_counters;
     // spp 4 (the reference's AA), 16 (configs c/d) and 64 (config e) have their own
     // instantiations: constant LDS offsets and it / spp, fewer scalar registers
+    // The reference's RECURSION_DEPTH (20, ao_compute.glsl:9) with bounce-ray clusters (every
+    // scene of 16..256 spheres) also has its own instantiations for spp 16 and 64: with the depth
+    // a constant and the rounds' plain full-scan fallback compiled out, fewer scalar registers are
+    // spilled to vector lanes (each reload is a v_readlane on the bounce rounds' path)
     if (!pl) {
-      if (p.spp == 16) launch_batch<16, false>(tl, cnt, g, b, psh, stream, q);
+      const bool ref_d = p.D == kRefDepth && p.ncl > 0;
+      if (p.spp == 16 && ref_d) launch_batch<16, false, kRefDepth, true>(tl, cnt, g, b, psh, stream, q);
+      else if (p.spp == 64 && ref_d) launch_batch<64, false, kRefDepth, true>(tl, cnt, g, b, psh, stream, q);
+      else if (p.spp == 16) launch_batch<16, false>(tl, cnt, g, b, psh, stream, q);
       else if (p.spp == 64) launch_batch<64, false>(tl, cnt, g, b, psh, stream, q);
       else if (p.spp == 4) launch_batch<4, false>(tl, cnt, g, b, psh, stream, q);
       else launch_batch<0, false>(tl, cnt, g, b, psh, stream, q);
