@@ -969,6 +969,11 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
     for (int k = lane; k < nobj; k += 64) geol[k] = geo[k];
     geol_valid = true;
   }
+  // the cluster table and masks (rt_kernels.h layout: shapes + 7S, i.e. geo + 3S) read through the
+  // read-only, non-aliased sphere-table pointer: their wave-uniform loads in the bounce rounds are
+  // then scalar loads (through FrameParams they were vector loads, one memory round trip each)
+  const float4* const clus = geo + (size_t)3 * P.S;
+  const unsigned long long* const clm = (const unsigned long long*)(geo + (size_t)3 * P.S + kMaxClusters);
   // col[ind] / aux[ind] (rt_device.h scene tables) addressed from the sphere table (geo = shapes + 4S, launch_program) with a
   // per-lane offset the compiler cannot fold into a hoisted pointer: the two extra 64-bit base
   // pointers were the most reloaded of the kernel's scalar spills (a v_readlane pair each, per shade)
@@ -1125,11 +1130,11 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   auto shade = [&](int ind, float t, f3& ps, f3& dr, f3 hm, float& r, float& g, float& b, int dpt, int it,
                    bool first) -> bool {
     const int lp = div_spp(it), aa = it - lp * spp;
-    float4 att = P.bg;  // miss: background
+    // a miss (ind == -1) reads the background: the host stores it as the colour table's row -1
+    float4 att = col_at(ind);
     int kind = PRIM_MISS;
     bool go = false;
     if (ind != -1) {
-      att = col_at(ind);
       const float4 ax = aux_at(ind);
       // all-sphere scenes: the hit sphere's centre requested with its colour and flags, one memory
       // round trip (pinned here: the compiler would sink the load behind the emissive test)
@@ -1403,7 +1408,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         unsigned long long kc = 0;
         for (int c0 = 0; c0 < P.ncl; c0 += G) {
           const int c = c0 + pl;
-          const bool may = act && c < P.ncl && cluster_may_hit(o, d, P.clus[c]);
+          const bool may = act && c < P.ncl && cluster_may_hit(o, d, clus[c]);
           unsigned long long b = __builtin_amdgcn_ballot_w64(may);
           for (int sh = 32; sh >= G; sh >>= 1) b |= b >> sh;
           kc |= (G == 64 ? b : (b & ((1ull << G) - 1))) << c0;
@@ -1411,8 +1416,8 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         unsigned char* list = (unsigned char*)cmask;
         int cnt = 0;
         for (int w = 0; w < nwords; ++w) {
-          unsigned long long m = P.clmask[w];
-          for (unsigned long long k2 = kc; k2;) m |= P.clmask[(size_t)(1 + pop_lowest(k2)) * kClusterWords + w];
+          unsigned long long m = clm[w];
+          for (unsigned long long k2 = kc; k2;) m |= clm[(size_t)(1 + pop_lowest(k2)) * kClusterWords + w];
           const int ln = lane_id_here();
           if ((m >> ln) & 1ull)
             list[cnt + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
@@ -1421,11 +1426,17 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         }
         __syncthreads();  // the list is written (one wave per workgroup)
         exec_tests += (unsigned long long)((P.ncl + G - 1) / G + (cnt + G - 1) / G);
-        if (act)
+        if (act) {
+          // the next list entry is requested before this one's test: one LDS round trip per
+          // sphere (entry, then the sphere row) instead of two dependent ones
+          int i = list[pl < cnt ? pl : 0];
           for (int k = pl; k < cnt; k += G) {
-            const int i = list[k];
-            sphere_candidate(o, d, tgeo[i], i, 0.0001f, t, ind);
+            const float4 g = tgeo[i];
+            const int inext = list[k + G < cnt ? k + G : cnt - 1];  // (no exec-mask branch around it)
+            sphere_candidate(o, d, g, i, 0.0001f, t, ind);
+            i = inext;
           }
+        }
       } else if (act) {
         for (int i = pl; i < nobj; i += G) sphere_candidate(o, d, tgeo[i], i, 0.0001f, t, ind);
       }
@@ -1465,16 +1476,34 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       // cluster cull: a cluster is skipped when no live lane's ray may hit it (cluster_may_hit);
       // the spheres of the kept clusters plus the always-tested ones are visited in ascending
       // index order, so (t, ind) is the full scan's (ao_compute.glsl:183-194)
+      // Four clusters per step, their records requested together (one scalar-load round trip per
+      // four; slots past ncl are still inside the table, the cluster masks follow the 64 slots,
+      // and their bits are dropped below).  Every lane tests (a lane without a path only sets a
+      // bit that the live mask drops), so the loop runs with the full exec mask.
       unsigned long long kc = 0;
-      for (int c = 0; c < P.ncl; ++c) {
-        const bool may = has && cluster_may_hit(pos, dir, P.clus[c]);
-        if (__builtin_amdgcn_ballot_w64(may) != 0) kc |= 1ull << c;
+      for (int c = 0; c < P.ncl; c += 4) {
+        const float4 c0 = clus[c], c1 = clus[c + 1], c2 = clus[c + 2], c3 = clus[c + 3];
+        const unsigned long long b0 = __builtin_amdgcn_ballot_w64(cluster_may_hit(pos, dir, c0)) & hm;
+        const unsigned long long b1 = __builtin_amdgcn_ballot_w64(cluster_may_hit(pos, dir, c1)) & hm;
+        const unsigned long long b2 = __builtin_amdgcn_ballot_w64(cluster_may_hit(pos, dir, c2)) & hm;
+        const unsigned long long b3 = __builtin_amdgcn_ballot_w64(cluster_may_hit(pos, dir, c3)) & hm;
+        kc |= (unsigned long long)((b0 != 0) | (b1 != 0) << 1 | (b2 != 0) << 2 | (b3 != 0) << 3) << c;
       }
+      if (P.ncl < 64) kc &= (1ull << P.ncl) - 1;
       float t = -1.0f;
       int ind = -1;
       for (int w = 0; w < nwords; ++w) {
-        unsigned long long m = P.clmask[w];
-        for (unsigned long long k2 = kc; k2;) m |= P.clmask[(size_t)(1 + pop_lowest(k2)) * kClusterWords + w];
+        unsigned long long m = clm[w];
+        // the kept clusters' member words, up to four requested per round trip (a repeated index
+        // when fewer are left: the same word OR-ed twice)
+        for (unsigned long long k2 = kc; k2;) {
+          const int a = pop_lowest(k2);
+          const int b = k2 ? pop_lowest(k2) : a;
+          const int e = k2 ? pop_lowest(k2) : a;
+          const int f = k2 ? pop_lowest(k2) : a;
+          m |= clm[(size_t)(1 + a) * kClusterWords + w] | clm[(size_t)(1 + b) * kClusterWords + w] |
+               clm[(size_t)(1 + e) * kClusterWords + w] | clm[(size_t)(1 + f) * kClusterWords + w];
+        }
         exec_tests += (unsigned long long)__popcll(m);
         if (has) {
           // (streaming the word's 4-sphere groups with a per-nibble skip, or loading 4 survivors

@@ -137,7 +137,10 @@ int hip_fail(rt_ctx* c, hipError_t e) {
 
 size_t slot_elems(const rt_ctx* c) { return (size_t)c->band_rows * c->cfg.width; }
 // stride of the device shape tables (>= 1, so an empty scene still has valid pointers)
-int table_stride(const rt_ctx* c) { return std::max(1, c->cfg.num_shapes); }
+// One row per table beyond the shapes: the colour table's row -1 (the geo2 table's last row)
+// holds the background, so the AO kernel's shading reads a miss's attenuation as col[-1]
+// (rt_kernels_impl.h col_at) instead of keeping the background in scalar registers.
+int table_stride(const rt_ctx* c) { return std::max(1, c->cfg.num_shapes) + 1; }
 
 hipEvent_t get_event(rt_ctx* c) {
   if (!c->event_pool.empty()) {
@@ -792,6 +795,13 @@ int pack_header(rt_ctx* c, const float* h, float4* tab, int& nobj, int& nplanes,
       pln[2 * np + 1] = make_float4(s[12], s[13], s[14], 0.0f);
       ++np;
     }
+  }
+  // the padding rows; the colour table's row -1 is the background (table_stride)
+  for (int k = 0; k < 4; ++k) tab[(size_t)k * Sc + Sc - 1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  tab[4 * (size_t)Sc + Sc - 1] = make_float4(qnan, qnan, qnan, qnan);  // sphere table: never accepted
+  {
+    const float* bg = h + RT_HDR_BACKGROUND * 4;
+    tab[(size_t)2 * Sc - 1] = make_float4(bg[0], bg[1], bg[2], bg[3]);
   }
   std::memcpy(tab + rt::rand_table(Sc), h + rt_off_rand(S) / 4, (size_t)2 * spp * sizeof(float4));
   nplanes = np;

@@ -1,0 +1,19 @@
+# r03ah: bounce rounds' cluster records and member masks as scalar loads through the sphere-table pointer,
+# full-exec cluster loop; c2 = two clusters per scalar load; bg = four per load, four member words per
+# round trip, background as the colour table row -1 (bg); new (in-tree) = bg + the split tail list entry read ahead; vs HEAD 6d4f894 (head)
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r03ah; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > $O/t.txt 2>&1 || { tail -30 $O/t.txt; exit 1; }; tail -1 $O/t.txt
+L=build/head/librtrt.so,build/c2/librtrt.so,build/bg/librtrt.so,real_time_ray_tracer_amd/librtrt.so
+for c in d c e; do
+timeout -k 10 300 python -u tools/ab.py --config $c --libs $L --rounds $([ $c = e ] && echo 3 || echo 8) --frames $([ $c = e ] && echo 2 || echo 6) --time-from 1 > $O/ab_ao_$c.txt 2>&1 || { tail -20 $O/ab_ao_$c.txt; exit 1; }
+tail -2 $O/ab_ao_$c.txt
+done
+for i in 1 2; do
+  for v in head c2 bg new; do
+    if [ $v = new ]; then unset RTRT_LIB; else export RTRT_LIB=build/$v/librtrt.so; fi
+    timeout -k 10 300 python -u bench.py --gpus 1 --steps 40 --warmup 5 --no-cpu-baseline > $O/bench_${v}_$i.json 2> $O/bench_${v}_$i.err || { tail $O/bench_${v}_$i.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_${v}_$i.json')); print('$v', $i, d['value'], d['ms_per_step'], d['ms_per_step_median'], d['roofline']['kernel_ms'], d['roofline_post']['kernel_ms'])"
+  done
+done
