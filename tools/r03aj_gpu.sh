@@ -1,0 +1,18 @@
+# r03aj: the first-bounce pre-test skip as a ballot branch + the cluster kept mask without the ncl mask
+# (var: build/var, commit a37c3f4, reverted pending this A/B) vs the in-tree build (99c084584b26)
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r03aj; mkdir -p $O
+RTRT_LIB=build/var/librtrt.so timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > $O/t.txt 2>&1 || { tail -30 $O/t.txt; exit 1; }; tail -1 $O/t.txt
+L=real_time_ray_tracer_amd/librtrt.so,build/var/librtrt.so
+for c in d c e; do
+timeout -k 10 300 python -u tools/ab.py --config $c --libs $L --rounds $([ $c = e ] && echo 3 || echo 8) --frames $([ $c = e ] && echo 2 || echo 6) --time-from 1 > $O/ab_ao_$c.txt 2>&1 || { tail -20 $O/ab_ao_$c.txt; exit 1; }
+tail -1 $O/ab_ao_$c.txt | cut -c1-400
+done
+for i in 1 2 3; do
+  for v in tree var; do
+    if [ $v = tree ]; then unset RTRT_LIB; else export RTRT_LIB=build/var/librtrt.so; fi
+    timeout -k 10 300 python -u bench.py --gpus 1 --steps 40 --warmup 5 --no-cpu-baseline > $O/bench_${v}_$i.json 2> $O/bench_${v}_$i.err || { tail $O/bench_${v}_$i.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_${v}_$i.json')); print('$v', $i, d['value'], d['ms_per_step'], d['ms_per_step_median'], d['roofline']['kernel_ms'], d['roofline_post']['kernel_ms'])"
+  done
+done
