@@ -284,6 +284,36 @@ __device__ __forceinline__ void sphere_candidate(f3 pos, f3 dir, float4 g, int i
   }
 }
 
+// sphere_candidate for the lanes with `on` only (the others run the arithmetic and accept nothing):
+// callers branch on a wave-uniform ballot of `on` instead of masking exec per lane.
+__device__ __forceinline__ void sphere_candidate_if(f3 pos, f3 dir, float4 g, int i, float thr, float& t, int& ind,
+                                                    bool on) {
+  f3 pmc = pos - xyz(g);
+  float b = dot(dir, pmc);
+  float del = fmaf(g.w, g.w, fmaf(b, b, -dot(pmc, pmc)));
+  const bool hit = on & (del >= 0.0f);
+  if (__builtin_amdgcn_ballot_w64(hit) != 0) {
+    // One straight-line tail for del == 0 and del > 0: with s = sqrt(0) = 0 both roots are
+    // -b, so the reference's (del == 0 ? -b : root choice) differs only in values <= 0, and
+    // (t2 < 0 ? t1 : t2) differs from (t2 < 0 ? (t1 < 0 ? -1 : t1) : t2) only when t1 < 0:
+    // none of these is ever accepted (thr > 0).  Accepted t and index are unchanged.
+    float s = thr >= 1e-6f ? sqrt_rn_tail(del) : sqrt_rn(del);  // thr is a literal at every call
+    float t1 = -1.0f * b + s;
+    float t2 = -1.0f * b - s;
+    // (t2 < 0 ? t1 : t2) as an unsigned min of the bits: t1 >= t2, so for t2 >= 0 both are
+    // non-negative and the min is t2; a negative t2 has its sign bit set and loses to t1 >= 0;
+    // the remaining cases (both negative, or t2 = -0 with t1 = +0) give a value <= 0 either
+    // way, which the acceptance below rejects (thr >= 0)
+    float res = __uint_as_float(min(__float_as_uint(t1), __float_as_uint(t2)));
+    // (res < t || t < 0) as one unsigned compare: t is -1.0f (no hit yet, bits 0xBF800000, above
+    // every positive float's bits, +inf included) or an accepted res > thr >= 0; for res > thr
+    // (positive, not NaN) and positive t the float and bit orders agree
+    const bool acc = hit & (res > thr) & (__float_as_uint(res) < __float_as_uint(t));  // no short-circuit branches
+    t = acc ? res : t;
+    ind = acc ? i : ind;
+  }
+}
+
 // The lowest set bit of a wave-uniform 64-bit mask, cleared with one s_bitset0_b64 (the
 // compiler's m & (m - 1) is a 64-bit subtract and an and: three scalar instructions).
 __device__ __forceinline__ int pop_lowest(unsigned long long& m) {

@@ -1306,8 +1306,9 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
                   tsec[0] += 1; tsec[1] += pm != 0; tsec[2] += dm != 0;
                   tsec[3] += (unsigned long long)__popcll(pm);
                 }
-                if (fmaf(bdir.z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w)
-                  sphere_candidate(bpos, bdir, g, k, 0.0001f, t, ind);
+                // the skip as a branch on the ballot (VCC), not an exec-mask save / restore per survivor
+                const bool pass = fmaf(bdir.z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w;
+                if (__builtin_amdgcn_ballot_w64(pass) != 0) sphere_candidate_if(bpos, bdir, g, k, 0.0001f, t, ind, pass);
               }
             if (ABL == 6) lap(6);
           } else if (live) {
@@ -1489,7 +1490,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         const unsigned long long b3 = __builtin_amdgcn_ballot_w64(cluster_may_hit(pos, dir, c3)) & hm;
         kc |= (unsigned long long)((b0 != 0) | (b1 != 0) << 1 | (b2 != 0) << 2 | (b3 != 0) << 3) << c;
       }
-      if (P.ncl < 64) kc &= (1ull << P.ncl) - 1;
+      // (bits of the slots past ncl need no mask: their member words are zero, rt_shim build_clusters)
       float t = -1.0f;
       int ind = -1;
       for (int w = 0; w < nwords; ++w) {
