@@ -13,6 +13,7 @@
  */
 #include "rt_oracle.h"
 
+#include <immintrin.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -90,6 +91,13 @@ typedef struct {
   int nobj;
   v3 horiz, vert, llc, cam, light;
   v4 bg;
+  /* the sphere geometry of shapes [0, nobj) as structure-of-arrays, padded to a multiple of 8
+     (NaN for non-spheres and padding: never accepted), and the indices of the planes: the
+     closest-hit scan evaluates 8 (AVX2) or 16 (AVX-512) spheres per step (closest_hit below) */
+  float* soa; /* [4][nsoa]: cx, cy, cz, r */
+  int nsoa;
+  int* planes;
+  int nplanes;
 } octx;
 
 #define SH(c, i, j, k) ((c)->shapes[((size_t)(i) * 5 + (j)) * 4 + (k)])
@@ -125,7 +133,37 @@ static int octx_init(octx* c, float* ssbo, const rto_dims* d, int frame) {
   c->bg.y = h[4 * RT_HDR_BACKGROUND + 1];
   c->bg.z = h[4 * RT_HDR_BACKGROUND + 2];
   c->bg.w = h[4 * RT_HDR_BACKGROUND + 3];
+  c->soa = NULL;
+  c->planes = NULL;
+  c->nsoa = c->nplanes = 0;
   return 0;
+}
+
+/* after octx_init: the structure-of-arrays sphere table and the plane list (freed by
+   octx_free).  Together they are eval_ray's dispatch on int(shapes[i][4].w)
+   (p_compute.glsl:121-138): id 1 = sphere_eval_ray, id 5 = plane_eval_ray, any other id
+   (rectangle 3 included) returns -1, i.e. is never accepted — a NaN row here.
+   Returns -1 when out of memory. */
+static int octx_tables(octx* c) {
+  int n8 = (c->nobj + 15) & ~15; /* a multiple of both vector widths */
+  c->nsoa = n8;
+  c->soa = (float*)malloc(sizeof(float) * 4 * (size_t)(n8 > 0 ? n8 : 1));
+  c->planes = (int*)malloc(sizeof(int) * (size_t)(c->nobj > 0 ? c->nobj : 1));
+  if (!c->soa || !c->planes) return -1;
+  for (int i = 0; i < n8; i++) {
+    int id = i < c->nobj ? (int)c->shapes[((size_t)i * 5 + 4) * 4 + 3] : -1;
+    for (int k = 0; k < 4; k++)
+      c->soa[(size_t)k * n8 + i] = id == RT_SHAPE_SPHERE ? c->shapes[(size_t)i * 5 * 4 + k] : NAN;
+    if (id == RT_SHAPE_PLANE) c->planes[c->nplanes++] = i;
+  }
+  return 0;
+}
+
+static void octx_free(octx* c) {
+  free(c->soa);
+  free(c->planes);
+  c->soa = NULL;
+  c->planes = NULL;
 }
 
 /* ------------------------------------------------------------------------------------ */
@@ -174,25 +212,118 @@ static float plane_eval(const octx* c, v3 pos, v3 dir, int i) {
   return dot3(n, sub3(p0, pos)) / denom;
 }
 
-static float eval_ray(const octx* c, v3 pos, v3 dir, int i) {
-  int id = (int)SH(c, i, 4, 3);
-  if (id == RT_SHAPE_SPHERE)
-    return sphere_eval(pos, dir, mk3(SH(c, i, 0, 0), SH(c, i, 0, 1), SH(c, i, 0, 2)), SH(c, i, 0, 3));
-  if (id == RT_SHAPE_PLANE) return plane_eval(c, pos, dir, i);
-  return -1.0f; /* rectangle and others are never hit (p_compute.glsl:132-137) */
+
+/* sphere_eval of spheres [i, i+8) of the SoA table, up to the values no caller accepts:
+   every caller accepts only res > thr >= 0, and this returns sphere_eval's value wherever that
+   is positive (del > 0: the same t2 / t1 choice; del == 0: -b - 0 = -b, and t1 = t2 when -b < 0;
+   del < 0 or NaN: NaN instead of -1).  Same binary32 operations in the same order, with the
+   hardware fma and IEEE sqrt, so the accepted values are bit-identical to sphere_eval's. */
+static inline __m256 sphere_eval8(const octx* c, int i, __m256 px, __m256 py, __m256 pz, __m256 dx, __m256 dy,
+                                  __m256 dz) {
+  const float* s = c->soa;
+  const size_t n = (size_t)c->nsoa;
+  __m256 mx = _mm256_sub_ps(px, _mm256_loadu_ps(s + i));
+  __m256 my = _mm256_sub_ps(py, _mm256_loadu_ps(s + n + i));
+  __m256 mz = _mm256_sub_ps(pz, _mm256_loadu_ps(s + 2 * n + i));
+  __m256 r = _mm256_loadu_ps(s + 3 * n + i);
+  __m256 b = _mm256_fmadd_ps(dz, mz, _mm256_fmadd_ps(dy, my, _mm256_mul_ps(dx, mx)));
+  __m256 pp = _mm256_fmadd_ps(mz, mz, _mm256_fmadd_ps(my, my, _mm256_mul_ps(mx, mx)));
+  __m256 del = _mm256_fmadd_ps(r, r, _mm256_fmsub_ps(b, b, pp)); /* fmaf(b, b, -pp): one rounding */
+  __m256 sq = _mm256_sqrt_ps(del);
+  __m256 nb = _mm256_mul_ps(_mm256_set1_ps(-1.0f), b);
+  __m256 t1 = _mm256_add_ps(nb, sq);
+  __m256 t2 = _mm256_sub_ps(nb, sq);
+  return _mm256_blendv_ps(t2, t1, _mm256_cmp_ps(t2, _mm256_setzero_ps(), _CMP_LT_OQ));
 }
 
-/* closest hit with threshold thr (p_compute.glsl:177-188; h_ 199-210; ao_ 183-194) */
+#ifdef __AVX512F__
+/* the same evaluation 16 spheres at a time (the CPU-baseline build for the GPU box's Zen 5
+   cores, -mavx512f): identical binary32 operations per lane */
+static inline __m512 sphere_eval16(const octx* c, int i, __m512 px, __m512 py, __m512 pz, __m512 dx, __m512 dy,
+                                   __m512 dz) {
+  const float* s = c->soa;
+  const size_t n = (size_t)c->nsoa;
+  __m512 mx = _mm512_sub_ps(px, _mm512_loadu_ps(s + i));
+  __m512 my = _mm512_sub_ps(py, _mm512_loadu_ps(s + n + i));
+  __m512 mz = _mm512_sub_ps(pz, _mm512_loadu_ps(s + 2 * n + i));
+  __m512 r = _mm512_loadu_ps(s + 3 * n + i);
+  __m512 b = _mm512_fmadd_ps(dz, mz, _mm512_fmadd_ps(dy, my, _mm512_mul_ps(dx, mx)));
+  __m512 pp = _mm512_fmadd_ps(mz, mz, _mm512_fmadd_ps(my, my, _mm512_mul_ps(mx, mx)));
+  __m512 del = _mm512_fmadd_ps(r, r, _mm512_fmsub_ps(b, b, pp));
+  __m512 sq = _mm512_sqrt_ps(del);
+  __m512 nb = _mm512_mul_ps(_mm512_set1_ps(-1.0f), b);
+  __m512 t1 = _mm512_add_ps(nb, sq);
+  __m512 t2 = _mm512_sub_ps(nb, sq);
+  return _mm512_mask_blend_ps(_mm512_cmp_ps_mask(t2, _mm512_setzero_ps(), _CMP_LT_OQ), t2, t1);
+}
+#endif
+
+/* closest hit with threshold thr (p_compute.glsl:177-188; h_ 199-210; ao_ 183-194).  The
+   reference's ascending scan `if (res > thr && (res < t || t < 0)) {t = res; ind = i;}` keeps,
+   for thr >= 0, the smallest accepted res and among equal ones the lowest index: evaluated
+   here 8 (AVX2) or 16 (AVX-512) spheres at a time (each lane keeps its own first minimum,
+   lanes merged by the same rule), then the planes (scalar plane_eval), merged by that rule. */
 static int closest_hit(const octx* c, v3 pos, v3 dir, float thr, float* t_out) {
   float t = -1.0f;
   int ind = -1;
-  for (int i = 0; i < c->nobj; i++) {
-    float res = eval_ray(c, pos, dir, i);
-    if (res > thr) {
-      if (res < t || t < 0.0f) {
-        t = res;
-        ind = i;
+  if (c->nsoa > 0) {
+#ifdef __AVX512F__
+    enum { VW = 16 };
+    const __m512 px = _mm512_set1_ps(pos.x), py = _mm512_set1_ps(pos.y), pz = _mm512_set1_ps(pos.z);
+    const __m512 dx = _mm512_set1_ps(dir.x), dy = _mm512_set1_ps(dir.y), dz = _mm512_set1_ps(dir.z);
+    const __m512 vthr = _mm512_set1_ps(thr);
+    __m512 bt = _mm512_set1_ps(INFINITY);
+    __m512i bi = _mm512_set1_epi32(-1);
+    __m512i idx = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+    const __m512i step = _mm512_set1_epi32(VW);
+    for (int i = 0; i < c->nsoa; i += VW) {
+      __m512 res = sphere_eval16(c, i, px, py, pz, dx, dy, dz);
+      __mmask16 acc = _mm512_cmp_ps_mask(res, vthr, _CMP_GT_OQ);
+      __mmask16 none = _mm512_cmpeq_epi32_mask(bi, _mm512_set1_epi32(-1));
+      __mmask16 upd = acc & (_mm512_cmp_ps_mask(res, bt, _CMP_LT_OQ) | none);
+      bt = _mm512_mask_blend_ps(upd, bt, res);
+      bi = _mm512_mask_blend_epi32(upd, bi, idx);
+      idx = _mm512_add_epi32(idx, step);
+    }
+    float lt[VW];
+    int li[VW];
+    _mm512_storeu_ps(lt, bt);
+    _mm512_storeu_si512((void*)li, bi);
+#else
+    enum { VW = 8 };
+    const __m256 px = _mm256_set1_ps(pos.x), py = _mm256_set1_ps(pos.y), pz = _mm256_set1_ps(pos.z);
+    const __m256 dx = _mm256_set1_ps(dir.x), dy = _mm256_set1_ps(dir.y), dz = _mm256_set1_ps(dir.z);
+    const __m256 vthr = _mm256_set1_ps(thr);
+    __m256 bt = _mm256_set1_ps(INFINITY);
+    __m256i bi = _mm256_set1_epi32(-1);
+    __m256i idx = _mm256_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7);
+    const __m256i step = _mm256_set1_epi32(VW);
+    for (int i = 0; i < c->nsoa; i += VW) {
+      __m256 res = sphere_eval8(c, i, px, py, pz, dx, dy, dz);
+      __m256 acc = _mm256_cmp_ps(res, vthr, _CMP_GT_OQ);
+      __m256 none = _mm256_castsi256_ps(_mm256_cmpeq_epi32(bi, _mm256_set1_epi32(-1)));
+      __m256 upd = _mm256_and_ps(acc, _mm256_or_ps(_mm256_cmp_ps(res, bt, _CMP_LT_OQ), none));
+      bt = _mm256_blendv_ps(bt, res, upd);
+      bi = _mm256_castps_si256(_mm256_blendv_ps(_mm256_castsi256_ps(bi), _mm256_castsi256_ps(idx), upd));
+      idx = _mm256_add_epi32(idx, step);
+    }
+    float lt[VW];
+    int li[VW];
+    _mm256_storeu_ps(lt, bt);
+    _mm256_storeu_si256((__m256i*)li, bi);
+#endif
+    for (int l = 0; l < VW; l++)
+      if (li[l] >= 0 && (ind < 0 || lt[l] < t || (lt[l] == t && li[l] < ind))) {
+        t = lt[l];
+        ind = li[l];
       }
+  }
+  for (int k = 0; k < c->nplanes; k++) {
+    int i = c->planes[k];
+    float res = plane_eval(c, pos, dir, i);
+    if (res > thr && (ind < 0 || res < t || (res == t && i < ind))) {
+      t = res;
+      ind = i;
     }
   }
   *t_out = t;
@@ -212,11 +343,45 @@ static int shadow_ray(const octx* c, v3 pos) {
   v3 l = nrm3(lv);
   float len = sqrtf(dot3(lv, lv));
   v3 np = add3(pos, scl3(0.01f, l));
-  for (int i = 0; i < c->nobj; i++) {
-    double t = (double)eval_ray(c, np, l, i);
+  /* "some object occludes" does not depend on the scan order: spheres 8 or 16 at a time (the
+     accepted values are sphere_eval's, see sphere_eval8), then the planes */
+#ifdef __AVX512F__
+  enum { VW = 16 };
+  const __m512 px = _mm512_set1_ps(np.x), py = _mm512_set1_ps(np.y), pz = _mm512_set1_ps(np.z);
+  const __m512 dx = _mm512_set1_ps(l.x), dy = _mm512_set1_ps(l.y), dz = _mm512_set1_ps(l.z);
+  const __m512 vthr = _mm512_set1_ps(0.0001f);
+#else
+  enum { VW = 8 };
+  const __m256 px = _mm256_set1_ps(np.x), py = _mm256_set1_ps(np.y), pz = _mm256_set1_ps(np.z);
+  const __m256 dx = _mm256_set1_ps(l.x), dy = _mm256_set1_ps(l.y), dz = _mm256_set1_ps(l.z);
+  const __m256 vthr = _mm256_set1_ps(0.0001f);
+#endif
+  for (int i = 0; i < c->nsoa; i += VW) {
+    float rv[VW];
+#ifdef __AVX512F__
+    __m512 res = sphere_eval16(c, i, px, py, pz, dx, dy, dz);
+    int m = (int)_mm512_cmp_ps_mask(res, vthr, _CMP_GT_OQ);
+    if (!m) continue;
+    _mm512_storeu_ps(rv, res);
+#else
+    __m256 res = sphere_eval8(c, i, px, py, pz, dx, dy, dz);
+    int m = _mm256_movemask_ps(_mm256_cmp_ps(res, vthr, _CMP_GT_OQ));
+    if (!m) continue;
+    _mm256_storeu_ps(rv, res);
+#endif
+    for (int k = 0; k < VW; k++)
+      if (m >> k & 1) {
+        double t = (double)rv[k];
+        double ddx = t * (double)l.x, ddy = t * (double)l.y, ddz = t * (double)l.z;
+        double L = sqrt(fma(ddz, ddz, fma(ddy, ddy, ddx * ddx)));
+        if (L < (double)len) return 0;
+      }
+  }
+  for (int k = 0; k < c->nplanes; k++) {
+    double t = (double)plane_eval(c, np, l, c->planes[k]);
     if (t > (double)0.0001f) {
-      double dx = t * (double)l.x, dy = t * (double)l.y, dz = t * (double)l.z;
-      double L = sqrt(fma(dz, dz, fma(dy, dy, dx * dx)));
+      double ddx = t * (double)l.x, ddy = t * (double)l.y, ddz = t * (double)l.z;
+      double L = sqrt(fma(ddz, ddz, fma(ddy, ddy, ddx * ddx)));
       if (L < (double)len) return 0;
     }
   }
@@ -605,6 +770,10 @@ int rto_run_program_window(float* ssbo, const rto_dims* d, int program, int fram
     free(snap);
     return 0;
   }
+  if (octx_tables(&c) != 0) {
+    octx_free(&c);
+    return -1;
+  }
   const long long w = x1 - x0, npx = w * (long long)(y1 - y0);
 #ifdef _OPENMP
 #pragma omp parallel for schedule(dynamic, 64) num_threads(nt)
@@ -619,6 +788,7 @@ int rto_run_program_window(float* ssbo, const rto_dims* d, int program, int fram
       default: break;
     }
   }
+  octx_free(&c);
   return 0;
 }
 

@@ -2,6 +2,13 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+// Normals slot layout, shared by the kernels and the shim (rt_download_rect reads the slots
+// directly): 1 = an xyz plane then a w plane (production), 0 = interleaved float4 (the round-2
+// layout, A/B builds only; set it for both translation units or neither).
+#ifndef RT_NRM_PLANES
+#define RT_NRM_PLANES 1
+#endif
+
 namespace rt {
 
 constexpr int kMaxFrames = 16;

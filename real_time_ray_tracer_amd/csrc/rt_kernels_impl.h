@@ -163,9 +163,6 @@ __device__ __forceinline__ float2 dep_load_xy(const float4* base, size_t off) { 
 // the pixel itself and its neighbours read both planes.  rt_download / rt_upload_gbuffer convert
 // to the reference's vec4 layout.
 // (RT_NRM_PLANES=0: interleaved float4, the round-2 layout, for A/B builds)
-#ifndef RT_NRM_PLANES
-#define RT_NRM_PLANES 1
-#endif
 __device__ __forceinline__ void nrm_store(float4* base, size_t n, size_t off, float4 v) {
   if (!RT_NRM_PLANES) {
     base[off] = v;

@@ -473,23 +473,35 @@ enum SlotKind { kPixels = 0, kNormals = 1, kDepth = 2 };
 // The g-buffer in the reference layout ([F][W][R] vec4, y fastest) goes through one device array
 // of that layout: a conversion kernel (rt::launch_gbuf_convert) between it and the slot layouts,
 // and one copy of exactly the caller's bytes (no host-side transposes).
+// The array holds ONE frame ([W][R] vec4): frames are converted and copied one at a time (each
+// frame is an independent [W][R] block of the reference layout), so a 4K context keeps 133 MB
+// for it, not the ring's F frames.
 int xfer_buffer(rt_ctx* c) {
-  if (!c->d_xfer) RT_HIP(c, hipMalloc(&c->d_xfer, (size_t)c->cfg.num_frames * c->cfg.width * c->own_rows * sizeof(float4)));
+  if (!c->d_xfer) {
+    hipError_t e = hipMalloc(&c->d_xfer, (size_t)c->cfg.width * c->own_rows * sizeof(float4));
+    if (e == hipErrorOutOfMemory) {
+      c->last_hip = (int)e;
+      c->d_xfer = nullptr;
+      return RT_E_NOMEM;
+    }
+    RT_HIP(c, e);
+  }
   return RT_OK;
 }
-rt::GbufXfer xfer_desc(const rt_ctx* c, int kind, int to_ref) {
+// frame f of array `kind` <-> the one-frame reference-layout array
+rt::GbufXfer xfer_desc(const rt_ctx* c, int kind, int to_ref, int f) {
   rt::GbufXfer x{};
   x.W = c->cfg.width;
   x.R = c->own_rows;
   x.r0 = c->own0 - c->band0;
-  x.F = c->cfg.num_frames;
+  x.F = 1;
   x.kind = kind;
   x.to_ref = to_ref;
   x.n = slot_elems(c);
   x.ref = c->d_xfer;
   const std::vector<float4*>& bufs = kind == kPixels ? c->pix : kind == kNormals ? c->nrm : c->dep;
   const std::vector<int>& map = kind == kPixels ? c->pix_slot : kind == kNormals ? c->nrm_slot : c->dep_slot;
-  for (int f = 0; f < x.F; ++f) x.slot[f] = bufs[map[f]];
+  x.slot[0] = bufs[map[f]];
   return x;
 }
 
@@ -1035,12 +1047,15 @@ int rt_download(rt_ctx* c, float* pixels, float* normals, float* depth, float* i
   if (rc == RT_OK) rc = sync_all(c);
   if (rc == RT_OK && (pixels || normals || depth)) rc = xfer_buffer(c);
   if (rc != RT_OK) return rc;
-  const size_t bytes = (size_t)c->cfg.num_frames * c->cfg.width * c->own_rows * sizeof(float4);
+  const size_t fbytes = (size_t)c->cfg.width * c->own_rows * sizeof(float4);  // one frame
   float* dst[3] = {pixels, normals, depth};
   for (int k = 0; k < 3; ++k) {
     if (!dst[k]) continue;
-    RT_HIP(c, rt::launch_gbuf_convert(xfer_desc(c, k, 1), c->stream));
-    RT_HIP(c, hipMemcpyAsync(dst[k], c->d_xfer, bytes, hipMemcpyDeviceToHost, c->stream));
+    for (int f = 0; f < c->cfg.num_frames; ++f) {  // stream order: frame f's copy precedes f+1's convert
+      RT_HIP(c, rt::launch_gbuf_convert(xfer_desc(c, k, 1, f), c->stream));
+      RT_HIP(c, hipMemcpyAsync((char*)dst[k] + (size_t)f * fbytes, c->d_xfer, fbytes, hipMemcpyDeviceToHost,
+                               c->stream));
+    }
   }
   if (image)
     RT_HIP(c, hipMemcpyAsync(image, c->d_image, (size_t)c->own_rows * c->cfg.width * 16, hipMemcpyDeviceToHost,
@@ -1090,9 +1105,6 @@ int rt_download_rect(rt_ctx* c, int x0, int x1, int y0, int y1, float* pixels, f
     for (int k = 0; k < 3; ++k) {
       auto& it = items[k];
       if (!it.dst) continue;
-#ifndef RT_NRM_PLANES
-#define RT_NRM_PLANES 1
-#endif
       RT_HIP(c, (k == kPixels || (k == kNormals && !RT_NRM_PLANES)) ? rect(it.src, y0 - c->band0)
                                                                    : split_rect(it.src, y0 - c->band0, k == kNormals ? 3 : 2));
       float* out = it.dst + (size_t)f * w * h * 4;  // [w][h] vec4, y fastest (reference layout)
@@ -1114,12 +1126,15 @@ int rt_upload_gbuffer(rt_ctx* c, const float* pixels, const float* normals, cons
   if (rc == RT_OK) rc = sync_all(c);
   if (rc == RT_OK && (pixels || normals || depth)) rc = xfer_buffer(c);
   if (rc != RT_OK) return rc;
-  const size_t bytes = (size_t)c->cfg.num_frames * c->cfg.width * c->own_rows * sizeof(float4);
+  const size_t fbytes = (size_t)c->cfg.width * c->own_rows * sizeof(float4);  // one frame
   const float* src[3] = {pixels, normals, depth};
   for (int k = 0; k < 3; ++k) {  // (the halo rows of a strip keep their contents)
     if (!src[k]) continue;
-    RT_HIP(c, hipMemcpyAsync(c->d_xfer, src[k], bytes, hipMemcpyHostToDevice, c->stream));
-    RT_HIP(c, rt::launch_gbuf_convert(xfer_desc(c, k, 0), c->stream));
+    for (int f = 0; f < c->cfg.num_frames; ++f) {
+      RT_HIP(c, hipMemcpyAsync(c->d_xfer, (const char*)src[k] + (size_t)f * fbytes, fbytes, hipMemcpyHostToDevice,
+                               c->stream));
+      RT_HIP(c, rt::launch_gbuf_convert(xfer_desc(c, k, 0, f), c->stream));
+    }
   }
   RT_HIP(c, hipStreamSynchronize(c->stream));
   return RT_OK;

@@ -13,6 +13,22 @@ if str(ROOT) not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
     config.addinivalue_line("markers", "slow: long CPU test")
+    # the checker: on the GPU box's AMD EPYC (AVX-512) the oracle's Zen build, the same C source
+    # with 16-wide sphere scans (bit-identical to the portable AVX2 build; tests/test_oracle_cpu.py)
+    import oracle
+    oracle.select_native()
+
+
+def pytest_terminal_summary(terminalreporter):
+    """Durations of the long parity tests (whole frames, full strips), always printed."""
+    rows = []
+    for rep in terminalreporter.stats.get("passed", []) + terminalreporter.stats.get("failed", []):
+        if getattr(rep, "when", "") == "call" and rep.duration >= 5.0:
+            rows.append((rep.duration, rep.nodeid, rep.outcome))
+    if rows:
+        terminalreporter.write_line(f"tests over 5 s ({len(rows)}):")
+        for dur, nid, out in sorted(rows, reverse=True):
+            terminalreporter.write_line(f"  {dur:7.1f} s  {out:6s} {nid}")
 
 
 def close(g, c, rel=1e-4, abs_=1e-6):

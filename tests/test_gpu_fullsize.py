@@ -4,8 +4,12 @@ The GPU renders the whole frame for a sequence of frames; the CPU oracle re-exec
 window of it on the same inputs and frame sequence:
   - 64x64 tiles chosen from the rendered image: the four corners, the flattest sky tile, the
     tile with the most silhouette edges, the brightest (emissive) tile and a ground tile;
-  - a full 270-row strip at config (d) (one eighth of the frame, the N = 8 strip height);
-  - config (a), the whole 640x480 frame.
+  - whole frames: config (a) 640x480, (b) and (c) 1920x1080 (3 frames each) and the headline
+    config (d) 3840x2160 over 10 pipelined frames (the temporal ring wraps);
+  - full strips: a 270-row strip of config (d) (one eighth of the frame, the N = 8 strip
+    height) and a 540-row strip of config (e) (8K, 256 spheres, 64 spp: the north star's
+    8-GPU config, one rank's strip) over 10 frames, so its ring wraps and frames 8 and 9 read
+    slots 0 and 1's stale depth (ao_compute.glsl:196-208).
 Trace passes run over the window plus a 1-pixel halo (the post-process reads its 4
 neighbours), the post-process over the window itself.  Normals and depth must agree bit for
 bit, colours within the north-star tolerance |g-c| <= 1e-4 max(|g|,|c|) + 1e-6 (conftest).
@@ -13,6 +17,9 @@ Mode-1 configs run >= 10 frames, so the 8-slot temporal ring (aop_postprocessing
 wraps and every history slot holds a filtered frame.  Plus size-independent properties of the
 whole frame: finite, non-negative, alpha 0.
 """
+import sys
+import time
+
 import numpy as np
 import pytest
 
@@ -72,7 +79,11 @@ def oracle_window(cfg: str, frames: int, x0: int, x1: int, y0: int, y1: int, mov
     img = np.zeros((gh, W, 4), np.float32)
     nt = oracle.nthreads_default()
     f = 0
+    t0 = time.perf_counter()
     for k in range(frames):
+        if k and (x1 - x0) * (y1 - y0) > 1 << 20:  # long oracle runs show progress (pytest -s)
+            print(f"  oracle {cfg} [{x0},{x1})x[{y0},{y1}): frame {k}/{frames}, {time.perf_counter() - t0:.1f} s",
+                  file=sys.stderr, flush=True)
         advance(h, mode, k, f, moving)
         buf[:h.data.size] = h.data
         for p in PROGS[mode]:
@@ -168,10 +179,40 @@ def test_full_size_tiles_moving_camera():
 
 
 def test_full_strip_config_d():
-    """One full N = 8 strip (rows [1080, 1350) of 2160) at config (d), 3 frames."""
-    r = gpu_render("d", 3, pipelined=True)
+    """One full N = 8 strip (rows [1080, 1350) of 2160) at config (d), 10 pipelined frames."""
+    r = gpu_render("d", 10, pipelined=True)
     W = CONFIGS["d"][0]
-    check_window(r, "d", 3, 0, W, 1080, 1350, "config (d) strip 4 of 8")
+    check_window(r, "d", 10, 0, W, 1080, 1350, "config (d) strip 4 of 8")
+    r.close()
+
+
+@pytest.mark.timeout(900)
+def test_full_strip_config_e():
+    """Config (e), 7680x4320, 256 spheres, AO 64 spp: one full N = 8 strip, rows [2160, 2700)
+    (540 rows: the strip of rank 4 of an equal 8-way split, through the horizon where ground,
+    spheres and sky meet), over 10 frames: the ring wraps, so frames 8 and 9 overwrite slots 0
+    and 1 and read their stale depth for emissive first hits.  The culls skip most of the
+    reference's tests here (>128-sphere global split tails, bounce-ray clusters); the oracle
+    runs the reference's brute-force scan."""
+    r = gpu_render("e", 10)
+    W = CONFIGS["e"][0]
+    check_window(r, "e", 10, 0, W, 2160, 2700, "config (e) strip 4 of 8")
+    r.close()
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cfg,frames,pipelined", [
+    ("b", 3, False),    # Phong + mirror bounces (<= 20), moving light (moving_light(true))
+    ("c", 3, False),    # AO 16 spp, 64 spheres
+    ("d", 10, True),    # the headline: AO 16 spp + post-process, pipelined, the ring wraps
+    ("e", 2, False),    # 8K, 256 spheres, AO 64 spp (the ring wrap: test_full_strip_config_e)
+])
+def test_whole_frame(cfg, frames, pipelined):
+    """The whole frame against the oracle: image, every ring slot's pixels (tolerance), and for
+    the AO modes every slot's normals and depth bit for bit."""
+    r = gpu_render(cfg, frames, pipelined)
+    W, H = CONFIGS[cfg][:2]
+    check_window(r, cfg, frames, 0, W, 0, H, f"config ({cfg}) whole frame")
     r.close()
 
 

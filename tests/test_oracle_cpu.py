@@ -5,6 +5,8 @@
     small frames for every program, built-in and synthetic scenes, multi-frame sequences;
   * the deterministic sin against numpy's libm sin.
 """
+import sys
+
 import numpy as np
 import pytest
 
@@ -162,3 +164,83 @@ def test_oracle_window_equals_whole_frame(mode):
         outs.append((img[y0:y1, x0:x1].copy(), ring.copy()))
     np.testing.assert_array_equal(outs[1][0].view(np.uint32), outs[0][0].view(np.uint32))
     np.testing.assert_array_equal(outs[1][1].view(np.uint32), outs[0][1].view(np.uint32))
+
+
+def _dup_scene(W, H, spp):
+    """24 synthetic spheres, then exact duplicates of some of them at indices that land in the
+    same lane of a later vector block (i + 8, i + 16) and in a neighbouring lane (i + 1): the
+    vectorised sphere scan (8 or 16 spheres per step) must keep the reference's lowest-index
+    winner of every tie (p_compute.glsl:177-188)."""
+    a = aspect_for(W, H)
+    base = Header.synthetic(24, spp, 1234, a, num_shapes=40)
+    h = base.copy()
+    shapes = h.data[28:28 + 40 * 20].reshape(40, 5, 4)
+    src = shapes[:24].copy()
+    order = list(range(24)) + [3, 1, 5, 9, 0, 4, 13, 2, 17, 6, 10, 11, 7, 12, 8, 14]
+    for i, j in enumerate(order):
+        shapes[i] = src[j]
+    h.set_mode(0, 40)
+    return h
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("scene", ["syn40", "dups"])
+def test_vector_scan_matches_numpy_restatement(scene, mode):
+    """The oracle's closest-hit and shadow scans run 8 (AVX2) or 16 (AVX-512) spheres per step
+    (rt_oracle.c closest_hit / shadow_ray); the numpy restatement scans one sphere at a time in
+    the reference's order.  Several vector blocks, padding, and ties across lanes and blocks."""
+    W, H, spp = 20, 16, 2
+    h = _dup_scene(W, H, spp) if scene == "dups" else _scene(scene, W, H, spp)
+    sc, sn = SSBO(h, W, H), SSBO(h, W, H)
+    d = oracle.dims(W, H, h.S, h.AA)
+    ic, inn = np.zeros((H, W, 4), np.float32), np.zeros((H, W, 4), np.float32)
+    f = 0
+    for k in range(2):
+        hk = h.copy()
+        hk.fill_rand_buffer(7000 + k) if mode in (1, 2) else hk.moving_light(True)
+        hk.set_mode(f, hk.num_objects)
+        sc.set_header(hk)
+        sn.set_header(hk)
+        oracle.dispatch(sc.data, d, mode, f, ic, nthreads=2)
+        f = numpy_ref.dispatch(sn.data, W, H, h.S, h.AA, mode, f, inn)
+    assert_close(inn, ic, f"{scene} mode {mode} image")
+    assert np.array_equal(sn.depth.view(np.uint32), sc.depth.view(np.uint32))
+    assert np.array_equal(sn.normals.view(np.uint32), sc.normals.view(np.uint32))
+
+
+def test_native_build_equals_portable_build():
+    """The oracle's two builds (x86-64-v3 AVX2, and the Zen AVX-512 build the GPU box's checker and
+    CPU baseline use) give bit-identical frames: same source, same binary32 operations."""
+    import subprocess
+    if not oracle.NATIVE_PATH.exists():
+        pytest.skip("no native build")
+    flags = open("/proc/cpuinfo").read()
+    if not all(f" {x}" in flags for x in ("avx512f", "avx512vl", "avx512bw", "avx512dq")):
+        pytest.skip("host has no AVX-512")
+    code = r'''
+import sys, numpy as np, ctypes as C
+sys.path.insert(0, sys.argv[1])
+import oracle
+oracle.LIB_PATH = oracle.NATIVE_PATH if sys.argv[2] == "native" else oracle.LIB_PATH
+from real_time_ray_tracer_amd import SSBO, Header, aspect_for
+W, H = 24, 18
+out = []
+for S, spp, mode in ((40, 3, 1), (37, 2, 2), (21, 1, 4), (19, 1, 3)):
+    h = Header.synthetic(S, spp, 99 + S, aspect_for(W, H))
+    s = SSBO(h, W, H); d = oracle.dims(W, H, h.S, h.AA); img = np.zeros((H, W, 4), np.float32); f = 0
+    for k in range(3):
+        hk = h.copy(); hk.fill_rand_buffer(7000 + k) if mode < 3 else hk.moving_light(True)
+        hk.set_mode(f, hk.num_objects); s.set_header(hk); f = oracle.dispatch(s.data, d, mode, f, img, nthreads=2)
+    out.append(s.data.view(np.uint32).copy()); out.append(img.view(np.uint32).copy())
+np.save(sys.argv[3], np.concatenate([o.ravel() for o in out]))
+'''
+    import tempfile
+    from pathlib import Path
+    root = str(Path(__file__).resolve().parents[1])
+    with tempfile.TemporaryDirectory() as td:
+        res = []
+        for which in ("portable", "native"):
+            p = f"{td}/{which}.npy"
+            subprocess.run([sys.executable, "-c", code, root, which, p], check=True)
+            res.append(np.load(p))
+    np.testing.assert_array_equal(res[0], res[1])

@@ -36,6 +36,25 @@ for d in sorted(glob.glob(os.path.join(out, f"{cfg}_g*"))):
                 name = k.replace("void ", "").replace("rt::(anonymous namespace)::", "").split("(rt::FrameParams")[0]
                 res[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 import json
+import shlex
+
+
+def frames_per_dispatch(cfg, bench_args):
+    """1 when every dispatch of the run renders one frame: mode 1 (the AO pass and the
+    post-process launch per frame) always; modes 2-4 only with --frame-batch 1 (the C++ frame
+    loop otherwise launches up to 8 frames at once).  None: several frames per dispatch."""
+    sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
+    from bench import CONFIGS
+    fb = None
+    a = shlex.split(bench_args)
+    for i, x in enumerate(a):
+        if x == "--frame-batch" and i + 1 < len(a):
+            fb = int(a[i + 1])
+        elif x.startswith("--frame-batch="):
+            fb = int(x.split("=", 1)[1])
+    return 1 if CONFIGS[cfg][4] == 1 or fb == 1 else None
+
+
 try:  # the library build the counters were taken on (make lib writes BUILD_INFO)
     info = json.load(open(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "real_time_ray_tracer_amd", "BUILD_INFO")))
 except Exception:
@@ -43,8 +62,7 @@ except Exception:
 out_json = {"config": cfg, "kernels": {}, "src_sha1": info.get("src_sha1"), "commit": info.get("commit"),
             "units": "per dispatch, mean over the dispatches of the bench run (warm-up, timed, standalone, counted)",
             "bench_args": os.environ.get("BENCH_ARGS", ""),
-            # one frame per dispatch: mode 1 always; modes 2-4 only with --frame-batch 1
-            "frames_per_dispatch": 1 if cfg in ("d", "p", "q", "s1") or "--frame-batch 1" in os.environ.get("BENCH_ARGS", "") else None}
+            "frames_per_dispatch": frames_per_dispatch(cfg, os.environ.get("BENCH_ARGS", ""))}
 for k, cs in res.items():
     avg = {c: round(sum(v) / len(v)) for c, v in sorted(cs.items())}
     print(cfg, k, avg, "dispatches", max(len(v) for v in cs.values()))
