@@ -43,7 +43,7 @@ $(LIB): $(OBJDIR)/rt_kernels.o $(OBJDIR)/rt_shim.o $(OBJDIR)/rt_host.o $(OBJDIR)
 	@src=$$(cat $(CSRC)/*.hip $(CSRC)/*.h $(CSRC)/rt_host.cpp $(CSRC)/rt_group.cpp include/rt/*.h Makefile | sha1sum | cut -c1-12); \
 	 commit=$$(git rev-parse --short=12 HEAD 2>/dev/null || echo unknown); \
 	 git diff --quiet HEAD -- $(CSRC) include Makefile 2>/dev/null || commit="$$commit+dirty"; \
-	 printf '{"src_sha1": "%s", "commit": "%s"}\n' "$$src" "$$commit" > $(PKG)/BUILD_INFO
+	 printf '{"src_sha1": "%s", "commit": "%s"}\n' "$$src" "$$commit" > $(dir $@)BUILD_INFO
 
 ABLIB := build/librtrt_ab.so
 $(OBJDIR)/rt_kernels_ab.o: tools/ab/rt_kernels_ab.hip $(CSRC)/*.h include/rt/*.h | $(OBJDIR)
@@ -53,6 +53,11 @@ $(ABLIB): $(OBJDIR)/rt_kernels_ab.o $(OBJDIR)/rt_shim.o $(OBJDIR)/rt_host.o $(OB
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 
 ablib: $(ABLIB)
+
+# A compile-time variant of the production library for tools/ab.py --libs (same sources, extra
+# defines):  make variant V=post32x8 VFLAGS="-DRT_POST_BWX=4 -DRT_POST_BWY=1"  -> build/v_post32x8/librtrt.so
+variant:
+	$(MAKE) lib OBJDIR=build/v_$(V)/obj LIB=build/v_$(V)/librtrt.so HIPFLAGS_EXTRA="$(VFLAGS)"
 
 $(ORACLE): oracle/rt_oracle.c oracle/rt_oracle.h include/rt/layout.h
 	@mkdir -p oracle/build
@@ -72,4 +77,4 @@ $(OBJDIR):
 clean:
 	rm -rf build oracle/build $(LIB)
 
-.PHONY: all lib oracle headless ablib clean
+.PHONY: all lib oracle headless ablib variant clean

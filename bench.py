@@ -95,46 +95,29 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cfg_name: str, target_s: float) -> dict:
-    """The CPU oracle (oracle/rt_oracle.c, OpenMP over rows) on a bounded, evenly spread sample
-    of rows of the same frame; both mode-1 passes for config (d)."""
-    import oracle
+def host_cpus() -> dict:
+    """The CPUs this process may use: the affinity mask, the cgroup CPU quota (the GPU box's
+    lease is 16 CPUs of a 256-CPU host: affinity shows all 256, the quota 16), and the thread
+    count the CPU baseline uses = min(affinity, quota)."""
+    import math
+    import shutil
+    import subprocess
 
-    oracle.select_native()
-    W, H, S, spp, mode, _ = CONFIGS[cfg_name]
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    h = config_header(cfg_name)
-    progs = {1: [oracle.AOP_COMPUTE, oracle.AOP_POSTPROCESSING], 2: [oracle.AO_COMPUTE],
-             3: [oracle.P_COMPUTE], 4: [oracle.H_COMPUTE]}[mode]
-
-    BAND, FR = 4, 2  # bands of 4 rows (vertical neighbours for the post-process), 2 frames each
-
-    def run_bands(starts):
-        t = 0.0
-        for y in starts:
-            gh = min(BAND, H - int(y))
-            d = oracle.dims(W, H, S, spp, gy0=int(y), gh=gh)
-            buf = np.zeros(h.data.size + 3 * 8 * W * gh * 4, np.float32)
-            hh = h.copy()
-            t0 = time.perf_counter()
-            for k in range(FR):  # the render loop's frames: history slot k-1 is filled
-                if mode in (1, 2):
-                    hh.fill_rand_buffer(7000 + k)
-                else:
-                    hh.moving_light(False)
-                hh.set_mode(k, hh.num_objects)
-                buf[:hh.data.size] = hh.data
-                for p in progs:
-                    oracle.run_program(buf, d, p, k, None, nthreads=threads)
-            t += time.perf_counter() - t0
-        return t
-
-    probe = run_bands([H // 2])
-    n = int(max(2, min(H // BAND, target_s / max(probe, 1e-4))))
-    starts = [min(H - BAND, int((i + 0.5) * H / n)) for i in range(n)]
-    t = run_bands(starts)
-    rows = [0] * (n * BAND)
-    units = len(rows) * W * (spp if mode in (1, 2) else 1) * FR
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    nproc = None
+    if shutil.which("nproc"):
+        try:  # GNU nproc honours OMP_NUM_THREADS; --all is the host's count
+            nproc = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
+        except ValueError:
+            pass
+    usable = aff if quota is None else max(1, min(aff, math.floor(quota + 1e-9)))
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -143,14 +126,90 @@ def cpu_baseline(cfg_name: str, target_s: float) -> dict:
                 break
     except OSError:
         pass
-    return {"value": round(units / t / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "cpu": model,
+    return {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "nproc": nproc, "os_cpu_count": os.cpu_count(),
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "usable": usable, "cpu": model}
+
+
+def cpu_baseline(cfg_name: str, target_s: float) -> dict:
+    """The CPU oracle (oracle/rt_oracle.c, OpenMP over pixels, one thread per usable CPU) on a
+    bounded, evenly spread sample of 4-row bands of the same frame.  Mode 1 is timed in steady
+    state: each band renders RING frames in a row (its 8-slot history ring fills), the AO pass
+    is timed in every frame and the post-process only once 7 history slots hold frames (the
+    temporal filter of aop_postprocessing.glsl:177-201 then examines up to 7 slots, as in the
+    GPU's timed frames); a frame costs the mean AO pass + the mean steady-state post-process."""
+    import oracle
+
+    oracle.select_native()
+    W, H, S, spp, mode, _ = CONFIGS[cfg_name]
+    cpus = host_cpus()
+    threads = cpus["usable"]
+    h = config_header(cfg_name)
+    progs = {1: [oracle.AOP_COMPUTE, oracle.AOP_POSTPROCESSING], 2: [oracle.AO_COMPUTE],
+             3: [oracle.P_COMPUTE], 4: [oracle.H_COMPUTE]}[mode]
+    BAND = 4                      # rows per band (vertical neighbours for the post-process)
+    FR = 9 if mode == 1 else 2    # frames per band: mode 1 -> frames 7 and 8 have 7 history slots
+    STEADY = 7                    # first steady-state frame of the post-process
+
+    def run_band(y):
+        """One band's FR frames: (trace s, trace passes, steady post s, steady post passes)."""
+        t_trace = t_post = 0.0
+        n_trace = n_post = 0
+        gh = min(BAND, H - int(y))
+        d = oracle.dims(W, H, S, spp, gy0=int(y), gh=gh)
+        buf = np.zeros(h.data.size + 3 * 8 * W * gh * 4, np.float32)
+        hh = h.copy()
+        for k in range(FR):
+            if mode in (1, 2):
+                hh.fill_rand_buffer(7000 + k)
+            else:
+                hh.moving_light(False)
+            slot = k % 8
+            hh.set_mode(slot, hh.num_objects)
+            buf[:hh.data.size] = hh.data
+            t0 = time.perf_counter()
+            oracle.run_program(buf, d, progs[0], slot, None, nthreads=threads)
+            t_trace += time.perf_counter() - t0
+            n_trace += 1
+            if mode == 1:
+                t0 = time.perf_counter()
+                oracle.run_program(buf, d, progs[1], slot, None, nthreads=threads)
+                if k >= STEADY:
+                    t_post += time.perf_counter() - t0
+                    n_post += 1
+        return t_trace, n_trace, t_post, n_post
+
+    # bands in van der Corput order over the frame's H / BAND bands (every prefix is spread
+    # evenly over the rows, sky and ground alike) until target_s of CPU work has run
+    nb = H // BAND
+    order, seen = [], set()
+    bits = max(1, (nb - 1).bit_length())
+    for i in range(1 << bits):
+        j = int(format(i, f"0{bits}b")[::-1], 2)
+        if j < nb and j not in seen:
+            seen.add(j)
+            order.append(j)
+    t_trace = t_post = 0.0
+    n_trace = n_post = n = 0
+    tw = time.perf_counter()
+    for j in order:
+        a, b_, c_, d_ = run_band(j * BAND)
+        t_trace, n_trace, t_post, n_post, n = t_trace + a, n_trace + b_, t_post + c_, n_post + d_, n + 1
+        if time.perf_counter() - tw >= target_s and n >= 2:
+            break
+    wall = time.perf_counter() - tw
+    per_band_frame = t_trace / n_trace + (t_post / n_post if n_post else 0.0)  # seconds per band per frame
+    rays = BAND * W * (spp if mode in (1, 2) else 1)                          # per band per frame
+    names = {1: "aop_compute", 2: "aop_postprocessing", 3: "ao_compute", 4: "p_compute", 5: "h_compute"}
+    return {"value": round(rays / per_band_frame / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "cpu": cpus["cpu"], "host_cpus": cpus,
+            "cores_note": ("threads = min(affinity CPUs, cgroup CPU quota): the lease's CPU share; more threads "
+                           "than the quota only time-slice"),
             "build": oracle.lib_name(),
-            "sample": f"{n} bands of {BAND} rows (evenly spread, {len(rows)} of {H} rows) x {FR} frames x {W} px x "
-                      f"{spp if mode in (1, 2) else 1} spp, "
-                      f"{'+'.join({1: 'aop_compute', 2: 'aop_postprocessing', 3: 'ao_compute', 4: 'p_compute', 5: 'h_compute'}[p] for p in progs)}, "
-                      f"oracle/rt_oracle.c with {threads} OpenMP threads, {t:.1f} s; ms/frame extrapolated "
-                      f"{t / (len(rows) * FR) * H * 1e3:.0f}"}
+            "sample": f"{n} bands of {BAND} rows (evenly spread, {n * BAND} of {H} rows) x {W} px x "
+                      f"{spp if mode in (1, 2) else 1} spp, {FR} frames per band"
+                      + (f" (post-process timed in frames {STEADY}-{FR - 1}, full history ring)" if mode == 1 else "")
+                      + f", {'+'.join(names[p] for p in progs)}, oracle/rt_oracle.c with {threads} OpenMP threads, "
+                      f"{wall:.1f} s; ms/frame extrapolated {per_band_frame * H / BAND * 1e3:.0f}"}
 
 
 def ssbo_path(cfg_name: str, gpu: int, frames: int = 30) -> dict:
@@ -253,12 +312,18 @@ def main():
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 also renders every frame whole and checks the gathered frames bit for bit "
                          "(without it, N > 1 still checks the first 2 gathered frames, before the timed region)")
-    ap.add_argument("--frame-batch", type=int, default=0,
-                    help="modes 2-4: most frames per launch in the C++ frame loop (rt_set_frame_batch); 0 = the "
-                         "library's default (multi-frame launches); 1 = one launch per frame, the form the "
-                         "committed per-frame PMC / SQ counter runs use (tools/pmc_config.sh BENCH_ARGS)")
+    ap.add_argument("--frame-batch", type=int, default=1,
+                    help="modes 2-4: most frames per launch in the C++ frame loop (rt_set_frame_batch).  1 (the "
+                         "default) = the reference's dispatch shape, one launch and one image write per frame "
+                         "(src/main.cpp:604): `value`.  >1: multi-frame launches (only the launch's last frame "
+                         "writes the image) are timed instead; either way the other shape is reported beside it")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N>1 path with ranks sharing GPUs, gather staged through host")
+    ap.add_argument("--dist-timeout", type=float, default=600.0,
+                    help="N>1: seconds a collective may wait for a peer before it raises (a rank that died "
+                         "takes the others down within this time instead of hanging the job)")
+    ap.add_argument("--inject-failure", type=int, default=-1, metavar="RANK",
+                    help="test hook: this rank raises right after the process group is up")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -271,14 +336,28 @@ def main():
     from real_time_ray_tracer_amd.dist import (StripGather, StripPlan, balanced_bounds, calibrate_row_cost, equal_bounds,
                                                imbalance)
 
+    from real_time_ray_tracer_amd.dist import init_process_group
+
+    # the process group first for gloo (no GPU call before its start-up check), after the
+    # device for RCCL (device_id binds the communicator); every collective times out after
+    # --dist-timeout, and run_rank (bottom) turns any exception into a named, non-zero exit
+    if world > 1 and args.backend == "gloo":
+        init_process_group("gloo", timeout_s=args.dist_timeout)
+    if world > 1 and args.backend == "nccl":
+        torch.cuda.set_device(local_rank)
+        init_process_group("nccl", torch.device("cuda", local_rank), timeout_s=args.dist_timeout)
+    if world > 1:
+        if rank == args.inject_failure:
+            raise RuntimeError(f"injected failure on rank {rank} (--inject-failure)")
+        # start-up check: every rank is alive and agrees on the run before any GPU work
+        chk = torch.tensor([1.0, float(args.steps)], dtype=torch.float64,
+                           device=torch.device("cuda", local_rank) if args.backend == "nccl" else "cpu")
+        dist.all_reduce(chk)
+        if int(chk[0].item()) != world or int(chk[1].item()) != world * args.steps:
+            raise RuntimeError(f"ranks disagree at start-up: {chk.tolist()} (world {world}, steps {args.steps})")
     gpu = local_rank if args.backend == "nccl" else local_rank % torch.cuda.device_count()
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
     cdev = dev if args.backend == "nccl" else torch.device("cpu")  # collective tensors
 
     W, H, S, spp, mode, desc = CONFIGS[args.config]
@@ -512,23 +591,30 @@ def main():
     progs = {1: [1, 2], 2: [3], 3: [4], 4: [5]}[mode]
     kstats = {p: rend.kernel_stats(p) for p in progs}
 
-    # ---- the reference's dispatch shape for the batched modes: one launch and one image write
-    # per frame (rt_set_frame_batch(1)), the same frames through the same C++ loop, wall clock --
-    per_frame = None
+    # ---- the other dispatch shape of modes 2-4, the same frames through the same C++ loop, wall
+    # clock: batched (up to F frames per launch, the image by each launch's last frame) beside
+    # the reference's one launch + one image write per frame, or the other way round --------
+    fb_timed = args.frame_batch
+    fb_other = 32 if fb_timed == 1 else 1
+    frames_per_launch = lambda fb: min(32, fb, rend.F)  # rt_compute_frames: min(kMaxBatch, batch, F)
+    other = None
     if host_loop and mode in (2, 3, 4):
-        rend.set_frame_batch(1)
-        # warm the single-frame path first (its kernel instantiation's first launches)
+        rend.set_frame_batch(fb_other)
+        # warm the other path first (its kernel instantiation's first launches)
         state["frame"] = rend.compute_frames(header, mode, state["frame"], 16, 7000 + warm, False)
         torch.cuda.synchronize()
         t0p = time.perf_counter()
         state["frame"] = rend.compute_frames(header, mode, state["frame"], args.steps, 7000 + warm, False)
         torch.cuda.synchronize()
         pf_s = (time.perf_counter() - t0p) / args.steps
-        rend.set_frame_batch(args.frame_batch if args.frame_batch > 0 else 32)
-        per_frame = {"ms_per_step": round(pf_s * 1e3, 4),
-                     "value": round(W * H * (spp if mode in (1, 2) else 1) / pf_s / 1e6, 2),
-                     "dispatch": "one launch and one image write per frame (rt_set_frame_batch(1)), C++ frame loop, "
-                                 "wall clock over the same number of frames"}
+        rend.set_frame_batch(fb_timed)
+        other = {"ms_per_step": round(pf_s * 1e3, 4),
+                 "value": round(W * H * (spp if mode in (1, 2) else 1) / pf_s / 1e6, 2),
+                 "frames_per_launch": frames_per_launch(fb_other),
+                 "dispatch": ("batched: up to %d frames per launch, each frame writing its own ring slot and the "
+                              "launch's last frame the image" % frames_per_launch(fb_other)) if fb_other > 1 else
+                             "one launch and one image write per frame (the reference's shape, src/main.cpp:604)",
+                 "measured": "C++ frame loop (rt_compute_frames), wall clock over the same number of frames"}
 
     # ---- standalone kernel times (two frames, not overlapped) and work counters (two more,
     # un-timed) on the timed frames' inputs -------------------------------------------------
@@ -549,6 +635,24 @@ def main():
         gather.finish()
     solo = {p: rend.kernel_stats(p) for p in progs}
     rend.enable_timing(False)
+    # mode 1's kernel durations the way rocprof's sequential run sees them: BURST back-to-back
+    # launches of one program on the stream, two events around the burst (no per-launch event,
+    # no other program between), the last rendered slot re-rendered with its own header (the AO
+    # pass rewrites identical values; a post-process re-filters its previous output: the same
+    # flag-, history- and byte-pattern, since those follow the normals and depth)
+    burst = {}
+    if mode == 1:
+        slot = (state["frame"] - 1) % rend.F
+        for prog, reps in ((1, 6), (2, 24)):
+            rend.run_program(prog, slot)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                rend.run_program(prog, slot)
+            e1.record(stream)
+            e1.synchronize()
+            burst[prog] = (e0.elapsed_time(e1) / reps, reps)
     rend.enable_counters(True)
     rend.read_counters(reset=True)
     ncount = 2
@@ -582,9 +686,11 @@ def main():
         n_l, tot = kstats[dom]
         timed_ms = tot / max(n_l, 1)
         solo_ms = solo[dom][1] / max(solo[dom][0], 1)
-        avg_ms = solo_ms if pipeline or host_loop else timed_ms
+        avg_ms = burst[dom][0] if dom in burst else solo_ms if pipeline or host_loop else timed_ms
         tests = counts["tests"] / ncount
-        tflops = FLOP_PER_TEST * tests / (avg_ms * 1e-3) / 1e12
+        exec_tests = counts["executed_lane_tests"] / ncount
+        eff_tflops = FLOP_PER_TEST * tests / (avg_ms * 1e-3) / 1e12
+        exec_tflops = FLOP_PER_TEST * exec_tests / (avg_ms * 1e-3) / 1e12
         sustained = FLOP_PER_TEST * tests / (elapsed / args.steps) / 1e12
         band_px = (r1 - r0 + (2 if mode in (1, 2) and world > 1 else 0)) * W
         hbm_alg = BYTES_PER_PIXEL[dom] * band_px / (avg_ms * 1e-3) / 1e9
@@ -594,50 +700,22 @@ def main():
         # a counter run's values are per dispatch: with multi-frame launches (modes 2-4 in the C++
         # loop) a dispatch holds up to F frames, so only runs taken one frame per dispatch
         # (--frame-batch 1, recorded as frames_per_dispatch) are comparable with a per-frame kernel_ms
-        per_dispatch_ok = lambda d: d is not None and (not host_loop or d.get("frames_per_dispatch") == 1)
+        per_frame_launches = not host_loop or fb_timed == 1
+        per_dispatch_ok = lambda d: d is not None and per_frame_launches and (
+            not host_loop or d.get("frames_per_dispatch") == 1)
         hw_note = None
         if traffic_data is not None and not per_dispatch_ok(traffic_data):
             hw_note = f"{traffic_src}: per multi-frame dispatch, not per frame; omitted"
             traffic_data, traffic_src = None, None
-        roof = {
-            "bound": "valu",
-            "achieved": round(tflops, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tflops / PEAK_FP32_TFLOPS, 4),
-            "traffic": traffic_data.get(str(dom)) if traffic_data else None,
-            "kernel": {1: "aop_compute (ao_kernel)", 3: "ao_compute (ao_kernel)", 4: "p_compute (phong_kernel)",
-                       5: "h_compute (hybrid_kernel)"}[dom],
-            "kernel_ms": round(avg_ms, 4),
-            "kernel_ms_measured": ("standalone launches (2 frames after the timed region); timed launches overlap"
-                                   if pipeline else "standalone launches (8 frames of the C++ loop after the timed region, "
-                                   "which runs without per-launch events; per frame)" if host_loop else "timed region"),
-            "kernel_ms_timed_span": None if pipeline or host_loop else round(timed_ms, 4),
-            "sustained_tflops_per_frame": round(sustained, 2),
-            "flop_per_launch": FLOP_PER_TEST * tests,
-            "tests_per_launch": tests,
-            "segments_per_sample": round(counts["segments"] / max(counts["samples"], 1), 4),
-            "useful_test_ratio": round(counts["tests"] / max(counts["executed_lane_tests"], 1), 4),
-            "basis": ("algorithmic: the reference's brute-force ray-shape tests (every segment tests every shape, "
-                      "20 FLOP each) per kernel second; the kernels skip provably missed tests (culling), so this "
-                      "can exceed the hardware peak when useful_test_ratio is high; valu_issue (when present) is "
-                      "the hardware's own view"),
-            "hbm": {"achieved": round(hbm_alg, 2), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                    "frac": round(hbm_alg / PEAK_HBM_GBPS, 6),
-                    "bytes_per_launch": BYTES_PER_PIXEL[dom] * band_px},
-            "traffic_source": traffic_src,
-            # the PMC run's library build vs this one: equal source hashes = measured on this kernel code
-            "traffic_src_sha1": traffic_data.get("src_sha1") if traffic_data else None,
-            "traffic_on_this_build": bool(traffic_data and traffic_data.get("src_sha1") == binfo.get("src_sha1")),
-        }
-        # the hardware's view beside the algorithmic one: VALU wave-instructions the kernel issues
-        # per launch (SQ_INSTS_VALU, committed counter run) over what the launch could issue at
-        # the spec rate (1 wave64 FP32 FMA per 2 clocks per SIMD, the peak above) and at the rate
-        # a dense v_fma_f32 stream sustains on this GPU
+        # the hardware's view: VALU wave-instructions the kernel issues per launch (SQ_INSTS_VALU,
+        # committed counter run of this library build) over what the launch could issue at the
+        # spec rate (one wave64 FP32 FMA, 128 FLOP, per 2 clocks per SIMD: the peak) and at the
+        # rate a dense v_fma_f32 stream sustains on this GPU
         sq, sq_src = load_sq(args.config, binfo.get("src_sha1")) if world == 1 else (None, None)
         if sq is not None and not per_dispatch_ok(sq):
             hw_note = (hw_note + "; " if hw_note else "") + f"{sq_src}: per multi-frame dispatch, not per frame; omitted"
             sq, sq_src = None, None
-        if hw_note:
-            roof["hardware_counters_note"] = hw_note
+        valu = None
         if sq:
             # the dominant program's kernel; of its instantiations the one with the most dispatches
             # (the timed form, not the counted one) where the file records dispatch counts
@@ -648,9 +726,63 @@ def main():
             insts = kern.get("SQ_INSTS_VALU")
             if insts:
                 spec = PEAK_FP32_TFLOPS * 1e12 / 128 * avg_ms * 1e-3
-                roof["valu_issue"] = {"insts_per_launch": insts, "frac_of_spec_issue": round(insts / spec, 4),
-                                      "frac_of_sustained_fma_issue": round(insts / (VALU_FMA_RATE * avg_ms * 1e-3), 4),
-                                      "source": sq_src, "on_this_build": sq.get("src_sha1") == binfo.get("src_sha1")}
+                valu = {"insts_per_launch": insts, "frac_of_spec_issue": round(insts / spec, 4),
+                        "frac_of_sustained_fma_issue": round(insts / (VALU_FMA_RATE * avg_ms * 1e-3), 4),
+                        "salu_insts_per_launch": kern.get("SQ_INSTS_SALU"),
+                        "source": sq_src, "on_this_build": sq.get("src_sha1") == binfo.get("src_sha1")}
+        # roofline on EXECUTED work: the VALU issue fraction of this build's counters (each wave64
+        # VALU instruction counted as one FMA's 128 FLOP, i.e. issue slots); without them, the
+        # lane-tests the kernel executes x 20 FLOP (a lower bound: per-sample setup, hashes and
+        # shading are not counted).  The reference's brute-force count is `effective_*`.
+        if valu and valu["on_this_build"]:
+            achieved = valu["insts_per_launch"] * 128 / (avg_ms * 1e-3) / 1e12
+            basis = ("executed: SQ_INSTS_VALU per launch (rocprofv3 --pmc run of this library build, %s) x 128 FLOP "
+                     "(one wave64 FMA per instruction = one issue slot) per kernel second; frac = VALU issue "
+                     "fraction of the spec peak" % sq_src)
+        else:
+            achieved = exec_tflops
+            basis = ("executed: lane-tests the kernel runs (work counters) x 20 FLOP per kernel second (no SQ "
+                     "counters of this build; a lower bound on executed work)")
+        roof = {
+            "bound": "valu",
+            "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+            "basis": basis,
+            "traffic": traffic_data.get(str(dom)) if traffic_data else None,
+            "kernel": {1: "aop_compute (ao_kernel)", 3: "ao_compute (ao_kernel)", 4: "p_compute (phong_kernel)",
+                       5: "h_compute (hybrid_kernel)"}[dom],
+            "kernel_ms": round(avg_ms, 4),
+            "kernel_ms_measured": (("%d back-to-back launches between two events after the timed region (the shape of "
+                                    "rocprof's sequential run); timed launches overlap when pipelined" % burst[dom][1])
+                                   if dom in burst else "standalone launches (8 frames of the C++ loop after the timed "
+                                   "region, which runs without per-launch events; per frame)" if host_loop else
+                                   "timed region"),
+            "kernel_ms_timed_span": None if pipeline or host_loop else round(timed_ms, 4),
+            "kernel_ms_standalone_events": round(solo_ms, 4),
+            "executed_test_tflops": round(exec_tflops, 2),
+            "executed_lane_tests_per_launch": exec_tests,
+            "effective_tflops": round(eff_tflops, 2),
+            "effective_frac": round(eff_tflops / PEAK_FP32_TFLOPS, 4),
+            "effective_basis": ("the reference's brute-force ray-shape tests (every segment tests every shape, 20 FLOP "
+                                "each) per kernel second: work the culled kernel does NOT execute "
+                                "(useful_test_ratio = brute-force / executed lane-tests), so it can exceed the peak"),
+            "sustained_effective_tflops_per_frame": round(sustained, 2),
+            "flop_per_launch_brute_force": FLOP_PER_TEST * tests,
+            "tests_per_launch": tests,
+            "segments_per_sample": round(counts["segments"] / max(counts["samples"], 1), 4),
+            "useful_test_ratio": round(counts["tests"] / max(counts["executed_lane_tests"], 1), 4),
+            "hbm": {"achieved": round(hbm_alg, 2), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                    "frac": round(hbm_alg / PEAK_HBM_GBPS, 6),
+                    "bytes_per_launch": BYTES_PER_PIXEL[dom] * band_px},
+            "traffic_source": traffic_src,
+            # the PMC run's library build vs this one: equal source hashes = measured on this kernel code
+            "traffic_src_sha1": traffic_data.get("src_sha1") if traffic_data else None,
+            "traffic_on_this_build": bool(traffic_data and traffic_data.get("src_sha1") == binfo.get("src_sha1")),
+        }
+        if hw_note:
+            roof["hardware_counters_note"] = hw_note
+        if valu:
+            roof["valu_issue"] = valu
         out = {
             "metric": "Mrays/s + ms/frame at 3840x2160, 16 AO samples, 64 spheres; 1/2/4/8 GPU",
             "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
@@ -668,8 +800,9 @@ def main():
                        + (", pipelined frames: consecutive AO passes on 2 alternating streams, post-process on a 3rd"
                           if pipeline else "")
                        + (", frame loop in C++ (rt_compute_frames)" if host_loop else "")
-                       + (", up to 8 frames per launch (each writes its colour slot; the image by the launch's "
-                          "last frame)" if host_loop and mode in (3, 4) else "")},
+                       + ((", one launch per frame" if fb_timed == 1 else
+                           ", up to %d frames per launch (each writes its colour slot; the image by the launch's "
+                           "last frame)" % frames_per_launch(fb_timed)) if host_loop and mode in (2, 3, 4) else "")},
             "roofline": roof,
             # host time per frame inside the frame calls = enqueue + waits for a free staging
             # buffer (back-pressure: the host runs up to 8 uploads ahead of the GPU)
@@ -677,11 +810,14 @@ def main():
             "host_backpressure_ms_per_step": round(host_wait_ms / args.steps, 4),
             "build": binfo,
         }
-        if per_frame is not None:
-            out["per_frame_dispatch"] = per_frame
-            out["dispatch"] = ("batched: up to 8 frames per launch, each frame writing its own ring slot and the "
-                               "launch's last frame the image (value and ms_per_step); per_frame_dispatch has the "
-                               "reference's one-launch-per-frame shape")
+        if host_loop and mode in (2, 3, 4):
+            out["dispatch"] = (("one launch and one image write per frame (rt_set_frame_batch(1)): the reference's "
+                                "dispatch shape (src/main.cpp:604)") if fb_timed == 1 else
+                               ("batched: up to %d frames per launch, each frame writing its own ring slot and the "
+                                "launch's last frame the image" % frames_per_launch(fb_timed)))
+            out["frames_per_launch"] = frames_per_launch(fb_timed)
+            if other is not None:
+                out["batched_dispatch" if fb_other > 1 else "per_frame_dispatch"] = other
         if balance_info is not None:
             sm = strip_ms.cpu().tolist()
             balance_info.update({"strip_ms": [round(t, 4) for t in sm], "imbalance": round(imbalance(sm), 4)})
@@ -697,8 +833,8 @@ def main():
         if mode == 1:
             # standalone launches: in the pipelined timed region the post-process shares the GPU
             # with the next frame's AO pass, so its event span is not a kernel duration
+            pms = burst[2][0]
             n_p, tot_p = solo[2]
-            pms = tot_p / max(n_p, 1)
             post_px = (r1 - r0) * W * ncount  # every pixel of the strip, per counted launch
             post_bytes = (POST_BYTES_PIXEL * post_px + POST_BYTES_FILTERED * counts["filtered_pixels"]
                           + POST_BYTES_SLOT_READ * counts["history_read"]
@@ -706,7 +842,10 @@ def main():
             pbw = post_bytes / (pms * 1e-3) / 1e9
             out["roofline_post"] = {"bound": "hbm", "achieved": round(pbw, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                                     "frac": round(pbw / PEAK_HBM_GBPS, 4), "kernel": "aop_postprocessing (post_kernel)",
-                                    "kernel_ms": round(pms, 4), "measured": "standalone (2 frames after the timed region)",
+                                    "kernel_ms": round(pms, 4),
+                                    "measured": ("%d back-to-back launches between two events after the timed region "
+                                                 "(the shape of rocprof's sequential run)" % burst[2][1]),
+                                    "kernel_ms_standalone_events": round(tot_p / max(n_p, 1), 4),
                                     "bytes_per_launch": round(post_bytes),
                                     "byte_model": "52 B/pixel + 20 B/filtered pixel + 20 B/history slot read + 16 B/slot accepted",
                                     "filtered_fraction": round(counts["filtered_pixels"] / max(post_px, 1), 4),
@@ -728,4 +867,6 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    from real_time_ray_tracer_amd.dist import run_rank
+
+    run_rank(main)

@@ -128,10 +128,11 @@ int rt_dispatch(rt_ctx* ctx, int mode, int frame);
  * Returns the next frame slot, or < 0. */
 int rt_compute_frames(rt_ctx* ctx, float* header, int mode, int frame, int n, uint64_t rand_seed,
                       int light_movement);
-/* rt_compute_frames renders modes 2-4 as launches of up to `max_frames` frames (default 32, at
- * most num_frames): each frame writes its own ring slot, the image is written by a launch's last
- * frame.  1 = one launch and one image write per frame, the reference's own dispatch shape
- * (src/main.cpp:604); the frames are identical either way. */
+/* rt_compute_frames renders modes 2-4 as launches of up to `max_frames` frames (at most
+ * num_frames).  1 (the default) = one launch and one image write per frame, the reference's own
+ * dispatch shape (src/main.cpp:604).  > 1 = multi-frame launches (opt-in): each frame writes its
+ * own ring slot, the image is written only by a launch's last frame (the one the caller sees).
+ * The ring, the image the caller sees and the header are identical either way. */
 int rt_set_frame_batch(rt_ctx* ctx, int max_frames);
 /* Copy device state to the host in the REFERENCE layout.  Any pointer may be NULL.
  * pixels/normals/depth: [F][W][R] vec4 (x-major, y fastest; R = rows of this context),

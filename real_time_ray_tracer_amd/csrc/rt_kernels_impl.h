@@ -1635,11 +1635,30 @@ __device__ __forceinline__ void xcd_tile(unsigned R, unsigned& bx, unsigned& by)
   bx = t - by * gx;
 }
 
+// Post-process tile shape: a wave covers kPostWX x (64 / kPostWX) pixels, a block kPostBWX x
+// kPostBWY waves (RT_POST_* overrides: A/B builds).
+#ifndef RT_POST_WX
+#define RT_POST_WX 8
+#endif
+#ifndef RT_POST_BWX
+#define RT_POST_BWX 2
+#endif
+#ifndef RT_POST_BWY
+#define RT_POST_BWY 2
+#endif
+constexpr int kPostWX = RT_POST_WX, kPostWY = 64 / RT_POST_WX, kPostBWX = RT_POST_BWX, kPostBWY = RT_POST_BWY;
+constexpr int kPostTileW = kPostWX * kPostBWX, kPostTileH = kPostWY * kPostBWY;
+static_assert(kPostWX * kPostWY == 64 && kPostBWX * kPostBWY * 64 == kBlock, "post tile shape");
+
 __global__ __launch_bounds__(kBlock) void post_kernel(FrameParams P) {
   int x, y;
   unsigned bx, by;
   xcd_tile((unsigned)P.tile_run, bx, by);
-  tile_xy<2, 2>(x, y, P.trace_row0, (int)bx, (int)by);
+  {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    x = (int)bx * kPostTileW + (wave % kPostBWX) * kPostWX + lane % kPostWX;
+    y = P.trace_row0 + (int)by * kPostTileH + (wave / kPostBWX) * kPostWY + lane / kPostWX;
+  }
   const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
   unsigned filtered = 0, visited = 0, accepted = 0;
   if (active) post_pixel(P, x, y, filtered, visited, accepted);
@@ -1916,12 +1935,15 @@ inline FrameParams launch_params(const FrameParams& p) {
   }
   {  // post-process XCD runs (xcd_tile): the least R in [4, gx / 16] dividing gx / 8 (a tile row
     // is a whole number of 8-run rounds, at least two per XCD), else 4; narrow frames: none
-    const int gx = (p.W + 15) / 16;
+    const int gx = (p.W + kPostTileW - 1) / kPostTileW;
     int R = 0;
     if (gx % 8 == 0)
       for (int r = 4; r <= gx / 16 && !R; ++r)
         if ((gx / 8) % r == 0) R = r;
     q.tile_run = R ? R : (gx >= 32 ? 4 : 0);
+#ifdef RT_POST_RUN
+    q.tile_run = RT_POST_RUN;  // A/B builds: a fixed run length (0 = row-major order)
+#endif
   }
   return q;
 }
@@ -1978,7 +2000,9 @@ inline hipError_t launch_production(int program, const FrameParams& p, const Fra
       else hipLaunchKernelGGL((hybrid_kernel<true, false, false>), grid, dim3(kBlock), 0, stream, q);
       break;
     case K_POST:
-      hipLaunchKernelGGL(post_kernel, grid, dim3(kBlock), 0, stream, q);
+      hipLaunchKernelGGL(post_kernel,
+                         dim3((p.W + kPostTileW - 1) / kPostTileW, (p.trace_rows + kPostTileH - 1) / kPostTileH),
+                         dim3(kBlock), 0, stream, q);
       break;
     default:
       return hipErrorInvalidValue;

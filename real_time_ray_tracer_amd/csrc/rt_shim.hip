@@ -98,7 +98,7 @@ struct rt_ctx {
   std::vector<float4> batch_host;
   std::vector<float> batch_hdr;  // the batch's host headers (camera, light: launch parameters)
   int nobj = 0;
-  int mf_max = rt::kMaxBatch;  // rt_compute_frames: most frames per launch (rt_set_frame_batch)
+  int mf_max = 1;  // rt_compute_frames: most frames per launch (rt_set_frame_batch; 1 = the reference's shape)
   Stage stage[kStageSlots];
   int stage_next = 0;
   // timing

@@ -152,3 +152,41 @@ class StripGather:
         if self.rank != self.root:
             return None
         return self.frames[k % self.nbuf]
+
+
+def init_process_group(backend: str, device=None, timeout_s: float = 300.0) -> None:
+    """torch.distributed.init_process_group with a finite timeout: every later collective of a
+    rank whose peer has died raises after timeout_s (gloo: the collective's own timeout; NCCL:
+    the watchdog), instead of blocking until an outside time limit kills the job."""
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    kw = {"timeout": timedelta(seconds=timeout_s)}
+    if backend == "nccl" and device is not None:
+        kw["device_id"] = device
+    dist.init_process_group(backend, **kw)
+
+
+def run_rank(fn, *args, **kwargs):
+    """Run one rank's body; on any exception print the rank and the error to stderr and exit
+    the process with status 1 at once (os._exit: no atexit / process-group teardown that could
+    block on dead peers).  The other ranks then fail at their next collective, within the
+    process group's timeout, and exit the same way, so a failed multi-GPU run ends with every
+    rank non-zero and the failing rank named."""
+    import os
+    import sys
+    import traceback
+
+    try:
+        return fn(*args, **kwargs)
+    except BaseException as e:  # noqa: BLE001 - every failure must end the rank loudly
+        if isinstance(e, SystemExit) and not e.code:
+            raise
+        rank = os.environ.get("RANK", "0")
+        world = os.environ.get("WORLD_SIZE", "1")
+        print(f"[rank {rank}/{world}] failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+        traceback.print_exc(file=sys.stderr)
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(1)

@@ -248,8 +248,9 @@ class Renderer:
                                                    int(bool(light_movement))), "rt_compute_frames")
 
     def set_frame_batch(self, max_frames: int):
-        """compute_frames' most frames per launch (modes 2-4); 1 = one launch and one image write
-        per frame, the reference's dispatch shape (rt_set_frame_batch)."""
+        """compute_frames' most frames per launch (modes 2-4); 1 (the default) = one launch and one
+        image write per frame, the reference's dispatch shape; > 1 = multi-frame launches, the image
+        by each launch's last frame (rt_set_frame_batch)."""
         self._c(self._lib.rt_set_frame_batch(self.ctx, int(max_frames)), "rt_set_frame_batch")
 
     def download(self, pixels=True, normals=True, depth=True, image=True) -> GBuffer:

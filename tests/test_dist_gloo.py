@@ -163,3 +163,67 @@ def test_c_planner_matches_numpy_restatement_and_rejects_bad_input():
     assert np.allclose(out[:4] / out[0], cost[:4] / cost[0])
     with pytest.raises(RtError):
         calibrate_row_cost([0, 4, 4, 10], cost, [1.0, 1.0, 1.0])
+
+
+def _failing_worker(rank, world, port, fail_rank, timeout_s):
+    """One rank of a calibration-like exchange under dist.run_rank: fail_rank raises before its
+    first collective, the others wait in an all_reduce for it."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from real_time_ray_tracer_amd.dist import init_process_group, run_rank
+
+    def body():
+        init_process_group("gloo", timeout_s=timeout_s)
+        if rank == fail_rank:
+            raise RuntimeError("simulated failure during strip calibration")
+        t = torch.zeros(world, dtype=torch.float64)
+        t[rank] = 1.0
+        dist.all_reduce(t)  # never completes: a peer is gone
+        return 0
+
+    run_rank(body)
+
+
+@pytest.mark.parametrize("fail_rank", [0, 1])
+def test_failed_rank_ends_every_rank_within_the_timeout(fail_rank):
+    """a rank that raises exits non-zero at once, naming itself; every other
+    rank's next collective raises within the process group's timeout and exits non-zero too, so
+    the job ends instead of hanging until an outside limit kills it."""
+    import time
+
+    ctx = mp.get_context("spawn")
+    world, timeout_s = 3, 8.0
+    port = _free_port()
+    t0 = time.time()
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, fail_rank, timeout_s)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    elapsed = time.time() - t0
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert all(c is not None and c != 0 for c in codes), codes
+    assert elapsed < timeout_s + 60, elapsed
+
+
+def test_bench_rank_failure_exits_nonzero_under_torchrun():
+    """bench.py itself as the driver launches it (torch.distributed.run, 2 ranks, gloo on the
+    CPU): rank 1 fails right after the process group is up (--inject-failure 1); the job exits
+    non-zero within the timeout and stderr names the failing rank."""
+    import subprocess
+    import sys
+    import time
+
+    port = _free_port()
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"),
+                        "--backend", "gloo", "--gpus", "2", "--steps", "2", "--inject-failure", "1",
+                        "--dist-timeout", "10"], capture_output=True, text=True, timeout=240, env=env, cwd=str(ROOT))
+    elapsed = time.time() - t0
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert "[rank 1/2] failed: RuntimeError: injected failure on rank 1" in r.stderr, r.stderr[-3000:]
+    assert elapsed < 200, elapsed

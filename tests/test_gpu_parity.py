@@ -111,7 +111,9 @@ def test_compute_frames_equals_frame_by_frame(mode, chunks):
     for many in (False, True, "one launch per frame"):
         r = Renderer(W, H, h.S, h.AA)
         if many == "one launch per frame":
-            r.set_frame_batch(1)  # rt_set_frame_batch: the reference's dispatch shape, same frames
+            r.set_frame_batch(1)  # rt_set_frame_batch: the reference's dispatch shape (the default)
+        elif many:
+            r.set_frame_batch(32)  # multi-frame launches (opt-in): the same frames
         hh = h.copy()
         drv = FrameDriver(r, hh, mode, light_movement=True)
         if many:

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # SQ counter passes for one bench config (one rocprofv3 --pmc run per counter group, no
 # tracing domains), summarised per kernel: tools/pmc_config.sh <tag> <config> [kernel-substring]
-# BENCH_ARGS: extra bench.py arguments (modes 2-4: "--frame-batch 1" for per-frame counters)
+# BENCH_ARGS: extra bench.py arguments (modes 2-4: bench.py launches one frame per dispatch by default)
 set -euo pipefail
 TAG=$1
 CFG=$2
@@ -41,11 +41,11 @@ import shlex
 
 def frames_per_dispatch(cfg, bench_args):
     """1 when every dispatch of the run renders one frame: mode 1 (the AO pass and the
-    post-process launch per frame) always; modes 2-4 only with --frame-batch 1 (the C++ frame
-    loop otherwise launches up to 8 frames at once).  None: several frames per dispatch."""
+    post-process launch per frame) always; modes 2-4 unless bench.py ran with --frame-batch > 1
+    (its default, 1, is one launch per frame).  None: several frames per dispatch."""
     sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
     from bench import CONFIGS
-    fb = None
+    fb = 1
     a = shlex.split(bench_args)
     for i, x in enumerate(a):
         if x == "--frame-batch" and i + 1 < len(a):

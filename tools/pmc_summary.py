@@ -40,6 +40,20 @@ def collect(d, counter, mode_cfg):
     return vals
 
 
+def frames_per_dispatch(mode_cfg, bench_args):
+    """1 when every dispatch renders one frame: mode 1 always; modes 2-4 unless bench.py ran
+    with --frame-batch > 1 (its default, 1, is one launch per frame).  None otherwise."""
+    import shlex
+    fb = 1
+    a = shlex.split(bench_args)
+    for i, x in enumerate(a):
+        if x == "--frame-batch" and i + 1 < len(a):
+            fb = int(a[i + 1])
+        elif x.startswith("--frame-batch="):
+            fb = int(x.split("=", 1)[1])
+    return 1 if mode_cfg == 1 or fb == 1 else None
+
+
 def main():
     fetch_dir, write_dir, cfg, out = sys.argv[1:5]
     mode_cfg = {"a": 3, "b": 4, "c": 2, "d": 1, "e": 2, "p": 1, "q": 1, "s1": 1}[cfg]
@@ -47,8 +61,7 @@ def main():
     wr = collect(write_dir, "WRITE_SIZE", mode_cfg)
     res = {"config": cfg, "units": "bytes per launch (FETCH_SIZE*2*1024 + WRITE_SIZE*1024, median)",
            "bench_args": os.environ.get("BENCH_ARGS", ""),
-           # one frame per dispatch: mode 1 always; modes 2-4 only with --frame-batch 1
-           "frames_per_dispatch": 1 if mode_cfg == 1 or "--frame-batch 1" in os.environ.get("BENCH_ARGS", "") else None}
+           "frames_per_dispatch": frames_per_dispatch(mode_cfg, os.environ.get("BENCH_ARGS", ""))}
     try:  # the library build the counters were taken on (make lib writes BUILD_INFO)
         info = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
                                            "real_time_ray_tracer_amd", "BUILD_INFO")))
