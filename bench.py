@@ -635,15 +635,19 @@ def main():
         gather.finish()
     solo = {p: rend.kernel_stats(p) for p in progs}
     rend.enable_timing(False)
-    # mode 1's kernel durations the way rocprof's sequential run sees them: BURST back-to-back
+    # kernel durations the way rocprof's sequential run sees them: a BURST of back-to-back
     # launches of one program on the stream, two events around the burst (no per-launch event,
-    # no other program between), the last rendered slot re-rendered with its own header (the AO
-    # pass rewrites identical values; a post-process re-filters its previous output: the same
-    # flag-, history- and byte-pattern, since those follow the normals and depth)
+    # no other program between; a per-launch event pair adds ~7 us, 20% of a config (b) frame),
+    # the last rendered slot re-rendered with its own header (a trace pass rewrites identical
+    # values; a post-process re-filters its previous output: the same flag-, history- and
+    # byte-pattern, since those follow the normals and depth)
     burst = {}
-    if mode == 1:
+    if True:
         slot = (state["frame"] - 1) % rend.F
-        for prog, reps in ((1, 6), (2, 24)):
+        # ~12 ms of launches per burst (AO at (d): 6, post: 24 ... hybrid at (b): 200)
+        reps_for = lambda p: int(min(400, max(6, 12.0 / max(solo[p][1] / max(solo[p][0], 1), 0.01))))
+        for prog in progs:
+            reps = reps_for(prog)
             rend.run_program(prog, slot)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -686,7 +690,7 @@ def main():
         n_l, tot = kstats[dom]
         timed_ms = tot / max(n_l, 1)
         solo_ms = solo[dom][1] / max(solo[dom][0], 1)
-        avg_ms = burst[dom][0] if dom in burst else solo_ms if pipeline or host_loop else timed_ms
+        avg_ms = burst[dom][0]
         tests = counts["tests"] / ncount
         exec_tests = counts["executed_lane_tests"] / ncount
         eff_tflops = FLOP_PER_TEST * tests / (avg_ms * 1e-3) / 1e12
@@ -752,11 +756,9 @@ def main():
             "kernel": {1: "aop_compute (ao_kernel)", 3: "ao_compute (ao_kernel)", 4: "p_compute (phong_kernel)",
                        5: "h_compute (hybrid_kernel)"}[dom],
             "kernel_ms": round(avg_ms, 4),
-            "kernel_ms_measured": (("%d back-to-back launches between two events after the timed region (the shape of "
-                                    "rocprof's sequential run); timed launches overlap when pipelined" % burst[dom][1])
-                                   if dom in burst else "standalone launches (8 frames of the C++ loop after the timed "
-                                   "region, which runs without per-launch events; per frame)" if host_loop else
-                                   "timed region"),
+            "kernel_ms_measured": ("%d back-to-back launches between two events after the timed region (the shape of "
+                                   "rocprof's sequential run; tools/burst_check.py compares the two)" % burst[dom][1]),
+            "burst_launches": burst[dom][1],
             "kernel_ms_timed_span": None if pipeline or host_loop else round(timed_ms, 4),
             "kernel_ms_standalone_events": round(solo_ms, 4),
             "executed_test_tflops": round(exec_tflops, 2),
@@ -845,6 +847,7 @@ def main():
                                     "kernel_ms": round(pms, 4),
                                     "measured": ("%d back-to-back launches between two events after the timed region "
                                                  "(the shape of rocprof's sequential run)" % burst[2][1]),
+                                    "burst_launches": burst[2][1],
                                     "kernel_ms_standalone_events": round(tot_p / max(n_p, 1), 4),
                                     "bytes_per_launch": round(post_bytes),
                                     "byte_model": "52 B/pixel + 20 B/filtered pixel + 20 B/history slot read + 16 B/slot accepted",

@@ -76,6 +76,21 @@ __device__ __forceinline__ float gclamp(float x, float lo, float hi) { return gm
 // ~5e5 at 8K).  GLSL leaves sin's precision for large arguments unspecified; what matters
 // for random() is that host and device compute the same value.
 __device__ __forceinline__ float det_sin(float x) {
+#if defined(RT_DETSIN) && RT_DETSIN == 2
+  // A/B candidate: one period reduction by 2 pi (3-part constant) and one odd degree-11
+  // polynomial on [-pi, pi] (|error| <= 4e-7): no quadrant, no second polynomial
+  const float k2 = rintf(x * 0.15915494f);
+  float r2 = fmaf(-k2, 6.2831855f, x);
+  r2 = fmaf(-k2, -1.7484555e-07f, r2);
+  r2 = fmaf(-k2, -6.860498e-15f, r2);
+  const float z2 = r2 * r2;
+  float p2 = fmaf(z2, -2.0366231e-08f, 2.6998227e-06f);
+  p2 = fmaf(z2, p2, -0.00019808741f);
+  p2 = fmaf(z2, p2, 0.008332408f);
+  p2 = fmaf(z2, p2, -0.16666554f);
+  p2 = fmaf(z2, p2, 0.9999996f);
+  return r2 * p2;
+#endif
   // (no explicit inf/NaN test: k = rint(+-inf) = +-inf makes r = NaN, and NaN stays NaN, so
   // both return NaN as the oracle's x - x does)
   float k = rintf(x * 0.636619772f);

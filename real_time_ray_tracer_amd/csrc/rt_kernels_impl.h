@@ -206,6 +206,10 @@ __device__ __forceinline__ FrameDst frame_dst(const FrameParams& P, int j) {
 // 4: -2.7%, 8: -17%; its waves are longer and the mirror bounces of a few tiles set the tail)
 // (tools/explore/r02m.sh).
 constexpr int kPhongFramesPerBlock = 4, kHybridFramesPerBlock = 1;
+#ifndef RT_HY_TPB
+#define RT_HY_TPB 1
+#endif
+constexpr int kHybridTilesPerBlock = RT_HY_TPB;  // 16x16 tiles per hybrid block, one after another
 template <int FPB>
 __device__ __forceinline__ int block_frames(const FrameParams& P, int& j0) {
   if (P.mf_n <= 0) {
@@ -862,7 +866,12 @@ __global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(FrameParams P) {
     else stage_shapes(P, lds);
     __syncthreads();
   }
-  if constexpr (kHybridFramesPerBlock == 1) {  // no frame loop (the loop form costs 3-4% at (b))
+  if constexpr (kHybridTilesPerBlock > 1) {  // A/B builds: TPB vertically adjacent tiles per block
+#pragma unroll 1
+    for (int t = 0; t < kHybridTilesPerBlock; ++t)
+      hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x,
+                                                 blockIdx.y * kHybridTilesPerBlock + t, frame_dst(P, blockIdx.z));
+  } else if constexpr (kHybridFramesPerBlock == 1) {  // no frame loop (the loop form costs 3-4% at (b))
     hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x, blockIdx.y,
                                                frame_dst(P, blockIdx.z));
   } else {
@@ -1982,7 +1991,8 @@ inline hipError_t launch_production(int program, const FrameParams& p, const Fra
   }
   // modes 3/4 multi-frame launches: FPB frames per block (block_frames)
   const int fpb = program == K_PHONG ? kPhongFramesPerBlock : kHybridFramesPerBlock;
-  dim3 grid((p.W + 15) / 16, (p.trace_rows + 15) / 16, p.mf_n > 0 ? (p.mf_n + fpb - 1) / fpb : 1);
+  const int tpb = program == K_HYBRID ? kHybridTilesPerBlock : 1;
+  dim3 grid((p.W + 15) / 16, ((p.trace_rows + 15) / 16 + tpb - 1) / tpb, p.mf_n > 0 ? (p.mf_n + fpb - 1) / fpb : 1);
   // scenes of at most kTabLdsMax objects: the tables staged in LDS per wave (LT)
   const bool lt = p.nobj <= kTabLdsMax;
   const size_t ltb = lt ? tab_lds_bytes(p) : 0;

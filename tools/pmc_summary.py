@@ -56,7 +56,9 @@ def frames_per_dispatch(mode_cfg, bench_args):
 
 def main():
     fetch_dir, write_dir, cfg, out = sys.argv[1:5]
-    mode_cfg = {"a": 3, "b": 4, "c": 2, "d": 1, "e": 2, "p": 1, "q": 1, "s1": 1}[cfg]
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from bench import CONFIGS
+    mode_cfg = CONFIGS[cfg][4]
     fe = collect(fetch_dir, "FETCH_SIZE", mode_cfg)
     wr = collect(write_dir, "WRITE_SIZE", mode_cfg)
     res = {"config": cfg, "units": "bytes per launch (FETCH_SIZE*2*1024 + WRITE_SIZE*1024, median)",
