@@ -43,21 +43,21 @@ def clamp(x, lo, hi):  # GLSL min(max(x, lo), hi) with GLSL's NaN-agnostic defin
 
 
 def det_sin(x):
+    """rt_oracle.c rto_sin: reduction by 2 pi (3-part constant), odd degree-11 polynomial."""
     x = np.asarray(x, F)
-    k = np.rint(x * F(0.636619772)).astype(F)
-    r = fma(-k, F(1.57079637), x)
-    r = fma(-k, F(-4.37113883e-08), r)
-    r = fma(-k, F(-1.71512451e-15), r)
-    # quadrant: integer k mod 4, k converted as v_cvt_i32_f32 (saturating beyond 2^31)
-    kf = np.where(np.isfinite(k), k, F(0.0)).astype(np.float64)
-    ki = np.clip(kf, -2.0 ** 31, 2.0 ** 31 - 1).astype(np.int64)
-    q = ki & 3
-    z = r * r
-    s = fma(r * z, fma(z, fma(z, F(-1.9515295891e-4), F(8.3321608736e-3)), F(-1.6666654611e-1)), r)
-    c = fma(z * z, fma(z, fma(z, F(2.443315711809948e-5), F(-1.388731625493765e-3)), F(4.166664568298827e-2)),
-            fma(F(-0.5), z, F(1.0)))
-    out = np.select([q == 0, q == 1, q == 2], [s, c, -s], -c).astype(F)
-    return np.where(np.isfinite(x), out, x - x)
+    h = lambda s: F(float.fromhex(s))  # noqa: E731
+    with np.errstate(invalid="ignore", over="ignore"):
+        k = np.rint(x * h("0x1.45f306p-3")).astype(F)
+        r = fma(-k, h("0x1.921fb6p+2"), x)
+        r = fma(-k, h("-0x1.777a5cp-23"), r)
+        r = fma(-k, h("-0x1.ee59dap-48"), r)
+        z = (r * r).astype(F)
+        p = fma(z, h("-0x1.5de3a2p-26"), h("0x1.6a5d34p-19"))
+        p = fma(z, p, h("-0x1.9f6b5ep-13"))
+        p = fma(z, p, h("0x1.11094ep-7"))
+        p = fma(z, p, h("-0x1.5554bep-3"))
+        p = fma(z, p, h("0x1.fffff2p-1"))
+        return (r * p).astype(F)
 
 
 def grandom(sx, sy):

@@ -49,24 +49,24 @@ static inline float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo
 
 /* ------------------------------------------------------------------------------------ */
 /* deterministic sin (the float semantics of random(); see rt_oracle.h)                 */
-/* binary32 Cody-Waite reduction by pi/2 with a 3-part constant and explicit fmaf, then   */
-/* the Cephes sinf/cosf polynomials (public domain minimax coefficients).                */
+/* one period reduction by 2 pi (a 3-part binary32 constant, explicit fmaf: r in          */
+/* [-pi, pi]) and one odd degree-11 minimax polynomial, |error| <= 4e-7 on [-pi, pi].     */
+/* GLSL leaves sin's precision implementation-defined (Vulkan's GLSL bound: 2^-11 on      */
+/* [-pi, pi], nothing beyond); what random() needs is that host and device agree.        */
 /* ------------------------------------------------------------------------------------ */
 float rto_sin(float x) {
-  if (!(fabsf(x) <= 3.40282347e38f)) return x - x; /* inf/nan -> nan */
-  float k = rintf(x * 0.636619772f);
-  float r = fmaf(-k, 1.57079637f, x);
-  r = fmaf(-k, -4.37113883e-08f, r);
-  r = fmaf(-k, -1.71512451e-15f, r);
-  /* quadrant: the integer k mod 4, with k converted as v_cvt_i32_f32 does (saturating beyond
-     2^31, where the quadrant is 3 for +k and 0 for -k); exact k mod 4 for |k| < 2^31 */
-  int32_t ki = k >= 2147483648.0f ? INT32_MAX : (k < -2147483648.0f ? INT32_MIN : (int32_t)k);
-  int q = (int)((uint32_t)ki & 3u);
+  /* inf/NaN: k = rint(+-inf) = +-inf makes r = NaN, so the result is NaN */
+  float k = rintf(x * 0x1.45f306p-3f);        /* x / 2pi */
+  float r = fmaf(-k, 0x1.921fb6p+2f, x);      /* 2pi = 0x1.921fb6p+2 - 0x1.777a5cp-23 - 0x1.ee59dap-48 */
+  r = fmaf(-k, -0x1.777a5cp-23f, r);
+  r = fmaf(-k, -0x1.ee59dap-48f, r);
   float z = r * r;
-  float s = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
-  float c = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
-                 fmaf(-0.5f, z, 1.0f));
-  return (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
+  float p = fmaf(z, -0x1.5de3a2p-26f, 0x1.6a5d34p-19f);
+  p = fmaf(z, p, -0x1.9f6b5ep-13f);
+  p = fmaf(z, p, 0x1.11094ep-7f);
+  p = fmaf(z, p, -0x1.5554bep-3f);
+  p = fmaf(z, p, 0x1.fffff2p-1f);
+  return r * p;
 }
 
 /* random(vec2) — p_compute.glsl:65-75: fract(sin(dot(st, vec2(12.9898,78.233))) * 43758.5453123) */

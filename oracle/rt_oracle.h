@@ -19,11 +19,11 @@
  *   - sphere discriminant = fmaf(r, r, fmaf(b, b, -dot(pmc,pmc)));
  *   - normalize(v) = v * (1.0f / sqrtf(dot(v,v))), length(v) = sqrtf(dot(v,v)), IEEE / and
  *     sqrtf (the correctly rounded form of the rsqrt-multiply GLSL compilers emit);
- *   - sin() inside random() = rto_sin(): binary32 Cody-Waite reduction by pi/2 (3-part
- *     constant, explicit fmaf) + Cephes sinf/cosf polynomials, quadrant = int32(k) & 3 with
- *     the conversion saturating beyond 2^31 (as v_cvt_i32_f32) — a deterministic sin (abs
- *     error ~1e-7 for |x| < 2^20) both sides reproduce bit for bit; random() only needs a
- *     deterministic hash, and GLSL leaves sin's large-argument precision unspecified;
+ *   - sin() inside random() = rto_sin(): one period reduction by 2 pi (a 3-part binary32
+ *     constant, explicit fmaf; r in [-pi, pi]) and one odd degree-11 minimax polynomial in
+ *     r^2 (|error| <= 4e-7 on [-pi, pi]) — a deterministic sin both sides reproduce bit for
+ *     bit; random() only needs a deterministic hash, and GLSL leaves sin's precision
+ *     implementation-defined (round 4; rounds 1-3 reduced by pi/2 with a quadrant select);
  *   - shadow_ray's `double t` and its dvec3 length run in binary64 (p_compute.glsl:147-163);
  *   - pow() = libm powf (outputs only; never feeds control flow), so pixels agree within
  *     the north-star tolerance |g-c| <= 1e-4*max(|g|,|c|) + 1e-6, not bit for bit.

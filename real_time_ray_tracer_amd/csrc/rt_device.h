@@ -3,7 +3,7 @@
 // Implements the float semantics documented in oracle/rt_oracle.h (the contract the CPU
 // oracle and these kernels share): IEEE binary32, no implicit contraction (the library is
 // built with -ffp-contract=off), dot() as a fused chain, normalize = v * (1/sqrtf(dot)), the
-// deterministic binary64 sin inside random(), binary64 shadow-ray distance test.
+// deterministic binary32 sin inside random(), binary64 shadow-ray distance test.
 // Reference: resources/p_compute.glsl:65-166, ao_compute.glsl:143-158.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -70,48 +70,26 @@ __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; 
 __device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
 __device__ __forceinline__ float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
 
-// ---- deterministic sin: binary32 Cody-Waite reduction by pi/2 (3-part constant, explicit
-// fmaf) + Cephes sinf/cosf minimax polynomials.  Bit-identical to oracle/rt_oracle.c rto_sin
-// for every float input; |error| ~ 1e-7 absolute for |x| < 2^20 (random() arguments reach
-// ~5e5 at 8K).  GLSL leaves sin's precision for large arguments unspecified; what matters
-// for random() is that host and device compute the same value.
+// ---- deterministic sin: one period reduction by 2 pi (3-part binary32 constant, explicit fmaf:
+// r in [-pi, pi]) and one odd degree-11 minimax polynomial (|error| <= 4e-7 on [-pi, pi]).
+// Bit-identical to oracle/rt_oracle.c rto_sin for every float input.  GLSL leaves sin's
+// precision implementation-defined (Vulkan's bound for GLSL: 2^-11 absolute on [-pi, pi]); what
+// matters for random() is that host and device compute the same value.  (Rounds 1-3 reduced by
+// pi/2 and evaluated the Cephes sin and cos polynomials with a quadrant select: 25 VALU per
+// random() against 17 here.)
 __device__ __forceinline__ float det_sin(float x) {
-#if defined(RT_DETSIN) && RT_DETSIN == 2
-  // A/B candidate: one period reduction by 2 pi (3-part constant) and one odd degree-11
-  // polynomial on [-pi, pi] (|error| <= 4e-7): no quadrant, no second polynomial
-  const float k2 = rintf(x * 0.15915494f);
-  float r2 = fmaf(-k2, 6.2831855f, x);
-  r2 = fmaf(-k2, -1.7484555e-07f, r2);
-  r2 = fmaf(-k2, -6.860498e-15f, r2);
-  const float z2 = r2 * r2;
-  float p2 = fmaf(z2, -2.0366231e-08f, 2.6998227e-06f);
-  p2 = fmaf(z2, p2, -0.00019808741f);
-  p2 = fmaf(z2, p2, 0.008332408f);
-  p2 = fmaf(z2, p2, -0.16666554f);
-  p2 = fmaf(z2, p2, 0.9999996f);
-  return r2 * p2;
-#endif
-  // (no explicit inf/NaN test: k = rint(+-inf) = +-inf makes r = NaN, and NaN stays NaN, so
-  // both return NaN as the oracle's x - x does)
-  float k = rintf(x * 0.636619772f);
-  float r = fmaf(-k, 1.57079637f, x);
-  r = fmaf(-k, -4.37113883e-08f, r);
-  r = fmaf(-k, -1.71512451e-15f, r);
-  // quadrant q = k mod 4 from the integer k (v_cvt_i32_f32 saturates beyond 2^31; the oracle
-  // mirrors that): bit 0 picks cos, bit 1 flips the sign, both read from k << 30
-  const int ki = (int)k;
-  const unsigned qs = (unsigned)ki << 30;
-  float z = r * r;
-  float s = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
-  float c = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
-                 fmaf(-0.5f, z, 1.0f));
-  // cos for odd k: the select as a bit mask (bit 0 of k sign-extended, v_bfe_i32) and a bitwise
-  // merge (v_bfi_b32), instead of an and, a compare into VCC (with its wait states) and a
-  // cndmask.  Written out: the compiler turns the C form back into the compare and cndmask.
-  unsigned sel, v;
-  asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(sel) : "v"(ki));
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(v) : "v"(sel), "v"(__float_as_uint(c)), "v"(__float_as_uint(s)));
-  return __uint_as_float(v ^ (qs & 0x80000000u));
+  // inf/NaN: k = rint(+-inf) = +-inf makes r = NaN, so the result is NaN (as the oracle's)
+  const float k = rintf(x * 0x1.45f306p-3f);
+  float r = fmaf(-k, 0x1.921fb6p+2f, x);
+  r = fmaf(-k, -0x1.777a5cp-23f, r);
+  r = fmaf(-k, -0x1.ee59dap-48f, r);
+  const float z = r * r;
+  float p = fmaf(z, -0x1.5de3a2p-26f, 0x1.6a5d34p-19f);
+  p = fmaf(z, p, -0x1.9f6b5ep-13f);
+  p = fmaf(z, p, 0x1.11094ep-7f);
+  p = fmaf(z, p, -0x1.5554bep-3f);
+  p = fmaf(z, p, 0x1.fffff2p-1f);
+  return r * p;
 }
 
 // IEEE binary32 square root, correctly rounded: the value sqrtf() has under
