@@ -319,6 +319,9 @@ def main():
                          "writes the image) are timed instead; either way the other shape is reported beside it")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N>1 path with ranks sharing GPUs, gather staged through host")
+    ap.add_argument("--no-alt-dispatch", action="store_true",
+                    help="modes 2-4: skip timing the other dispatch shape (counter runs: every dispatch then has "
+                         "the timed shape, so per-dispatch counters are per frame)")
     ap.add_argument("--dist-timeout", type=float, default=600.0,
                     help="N>1: seconds a collective may wait for a peer before it raises (a rank that died "
                          "takes the others down within this time instead of hanging the job)")
@@ -598,7 +601,7 @@ def main():
     fb_other = 32 if fb_timed == 1 else 1
     frames_per_launch = lambda fb: min(32, fb, rend.F)  # rt_compute_frames: min(kMaxBatch, batch, F)
     other = None
-    if host_loop and mode in (2, 3, 4):
+    if host_loop and mode in (2, 3, 4) and not args.no_alt_dispatch:
         rend.set_frame_batch(fb_other)
         # warm the other path first (its kernel instantiation's first launches)
         state["frame"] = rend.compute_frames(header, mode, state["frame"], 16, 7000 + warm, False)

@@ -20,7 +20,7 @@ for G in "$G1" "$G2" $([ -n "$G3" ] && echo "G3"); do
   [ "$G" = "G3" ] && G="$G3"
   i=$((i+1))
   timeout -k 10 120 rocprofv3 --pmc $G --output-format csv -d "$OUT/${CFG}_g$i" -o run -- \
-    python3 bench.py --config "$CFG" --steps 10 --warmup 8 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/${CFG}_g$i.log" 2>&1
+    python3 bench.py --config "$CFG" --steps 10 --warmup 8 --no-cpu-baseline --no-alt-dispatch ${BENCH_ARGS:-} > "$OUT/${CFG}_g$i.log" 2>&1
 done
 python3 - "$OUT" "$CFG" "$KSUB" <<'EOF'
 import csv, glob, os, sys, collections

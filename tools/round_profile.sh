@@ -17,9 +17,9 @@ ksub() { case $1 in a) echo phong_kernel;; b) echo hybrid_kernel;; *) echo ao_ba
 for c in "$@"; do
   if [ "$WHAT" = counters ]; then
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$c -o run -- \
-      python3 bench.py --config $c --steps 10 --no-cpu-baseline > /dev/null 2> $O/pmc_fetch_$c.err
+      python3 bench.py --config $c --steps 10 --no-cpu-baseline --no-alt-dispatch > /dev/null 2> $O/pmc_fetch_$c.err
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$c -o run -- \
-      python3 bench.py --config $c --steps 10 --no-cpu-baseline > /dev/null 2> $O/pmc_write_$c.err
+      python3 bench.py --config $c --steps 10 --no-cpu-baseline --no-alt-dispatch > /dev/null 2> $O/pmc_write_$c.err
     python3 tools/pmc_summary.py $O/pmc_fetch_$c $O/pmc_write_$c $c $O/pmc_$c.json
     timeout -k 10 900 bash tools/pmc_config.sh $TAG $c $(ksub $c) > $O/sq_$c.txt 2>&1
     tail -3 $O/sq_$c.txt
