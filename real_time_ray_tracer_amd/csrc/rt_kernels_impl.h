@@ -1699,15 +1699,20 @@ __device__ __forceinline__ void xcd_tile(unsigned R, unsigned& bx, unsigned& by)
 }
 
 // Post-process tile shape: a wave covers kPostWX x (64 / kPostWX) pixels, a block kPostBWX x
-// kPostBWY waves (RT_POST_* overrides: A/B builds).
+// kPostBWY waves (RT_POST_* overrides: A/B builds).  Round 4: a wave is one 64-pixel row segment
+// and a block 64 x 4 pixels (was 8 x 8 waves in 16 x 16 blocks): a wave's loads of an array are
+// then whole contiguous lines (1 KiB of colour, 768 B of normals, 512 B of depth), its left /
+// right neighbours are its own lanes' lines but for the two edge pixels, and the up / down rows
+// are the block's other waves'.  Config (d): 0.350 -> 0.300 ms per launch, same process
+// (128 x 2 blocks 0.317, row-major tile order 0.321; profiles/r04d_ab_post.txt)
 #ifndef RT_POST_WX
-#define RT_POST_WX 8
+#define RT_POST_WX 64
 #endif
 #ifndef RT_POST_BWX
-#define RT_POST_BWX 2
+#define RT_POST_BWX 1
 #endif
 #ifndef RT_POST_BWY
-#define RT_POST_BWY 2
+#define RT_POST_BWY 4
 #endif
 constexpr int kPostWX = RT_POST_WX, kPostWY = 64 / RT_POST_WX, kPostBWX = RT_POST_BWX, kPostBWY = RT_POST_BWY;
 constexpr int kPostTileW = kPostWX * kPostBWX, kPostTileH = kPostWY * kPostBWY;

@@ -93,7 +93,8 @@ struct rt_ctx {
   int nplanes = 0;             // planes among simple_shapes[0, nobj)
   int ncl = 0;                 // AO bounce-ray clusters of the table the next dispatch reads (build_clusters)
   float4* d_xfer = nullptr;    // rt_download / rt_upload_gbuffer: one array in the reference layout [F][W][R]
-  float4* d_batch = nullptr;   // rt_compute_frames: a batch of device table copies (one per frame)
+  float4* d_batch = nullptr;   // rt_compute_frames: device table copies, 2 x kBatch slots (one per distinct table)
+  int batch_last = -1;         // the d_batch slot d_shapes points into after rt_compute_frames (else -1)
   float4* d_mf_rb = nullptr;   // rt_compute_frames, mode 2: the rand_buffers of a multi-frame launch
   std::vector<float4> batch_host;
   std::vector<float> batch_hdr;  // the batch's host headers (camera, light: launch parameters)
@@ -655,6 +656,13 @@ int rt_enable_pipelining(rt_ctx* c, int on, void* output_stream) {
     c->out_stream = c->stream;
     return RT_OK;
   }
+  if (c->d_shapes && c->d_shapes != c->d_shapes_buf[0]) {
+    // the current table sits in an rt_compute_frames slot: pipelined frames read header copy k
+    RT_HIP(c, hipMemcpyAsync(c->d_shapes_buf[0], c->d_shapes, c->table.size() * sizeof(float4),
+                             hipMemcpyDeviceToDevice, c->stream));
+    c->d_shapes = c->d_shapes_buf[0];
+    c->d_rb = c->d_rb_buf[0];
+  }
   for (int k = 1; k < c->n_ao_streams; ++k)
     if (!c->ao_streams[k]) RT_HIP(c, hipStreamCreateWithFlags(&c->ao_streams[k], hipStreamNonBlocking));
   if (output_stream) {
@@ -985,35 +993,62 @@ int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint
     return frame;
   }
   // Sequential frames in batches: the host updates of up to kBatch frames are packed into
-  // consecutive device table copies with ONE upload, then the frames' programs are launched
-  // back to back, each reading its own copy.  Per frame the host then only enqueues kernels,
-  // which keeps small frames (config (a): a ~9 us kernel) GPU-bound.
+  // device table copies with ONE upload, then the frames' programs are launched back to back,
+  // each reading its own copy.  Per frame the host then only enqueues kernels, which keeps small
+  // frames (config (a): a ~9 us kernel) GPU-bound.  Only DISTINCT tables are uploaded: modes 3/4
+  // move the light, which travels in the kernel arguments, so their packed table never changes
+  // and, after the first call, nothing is copied at all (an in-stream host-to-device copy
+  // between two kernels stalls the queue for the copy's round trip: ~40 us every 8 frames of
+  // config (b), 5 us per frame).  The last table stays where it is (d_batch slot batch_last)
+  // as the context's current table.
   constexpr int kBatch = 32;
   const size_t tv = c->table.size();
   RT_HIP(c, hipSetDevice(c->device));
   int jr = join(c);
   if (jr != RT_OK) return jr;
-  if (!c->d_batch) RT_HIP(c, hipMalloc(&c->d_batch, (size_t)kBatch * tv * sizeof(float4)));
+  if (!c->d_batch) RT_HIP(c, hipMalloc(&c->d_batch, (size_t)2 * kBatch * tv * sizeof(float4)));
   c->batch_host.resize((size_t)kBatch * tv);
   c->batch_hdr.resize((size_t)kBatch * (bytes / sizeof(float)));
   const int Sc = table_stride(c);
   const size_t hf = bytes / sizeof(float);
+  const size_t tb = tv * sizeof(float4);
   for (int k0 = 0; k0 < n; k0 += kBatch) {
     const int m = std::min(kBatch, n - k0);
-    std::vector<int> nobj(m), npl(m), ncl(m), slot(m);
+    std::vector<int> nobj(m), npl(m), ncl(m), slot(m), dslot(m);
+    // the context's current table, if it already sits in a d_batch slot (host copy: c->table)
+    const int prev = (c->batch_last >= 0 && c->d_shapes == c->d_batch + (size_t)c->batch_last * tv) ? c->batch_last : -1;
+    int nd = 0;                  // distinct new tables, packed into batch_host[0 .. nd)
+    const float4* last = prev >= 0 ? c->table.data() : nullptr;  // the previous frame's table
     int f = frame;
     for (int j = 0; j < m; ++j) {
+      float4* tab = c->batch_host.data() + (size_t)nd * tv;
       int rc = update(k0 + j, f);
-      if (rc == RT_OK) rc = pack_header(c, header, c->batch_host.data() + (size_t)j * tv, nobj[j], npl[j], ncl[j]);
+      if (rc == RT_OK) rc = pack_header(c, header, tab, nobj[j], npl[j], ncl[j]);
       if (rc != RT_OK) return rc;
       std::memcpy(c->batch_hdr.data() + (size_t)j * hf, header, bytes);  // camera / light of frame j
       slot[j] = f;
       f = (f + 1) % c->cfg.num_frames;
+      if (last && std::memcmp(tab, last, tb) == 0) {
+        dslot[j] = j == 0 ? -1 : dslot[j - 1];  // -1: the previous slot `prev`
+      } else {
+        dslot[j] = -2 - nd;  // new table nd (its slot is fixed below)
+        last = tab;
+        ++nd;
+      }
     }
-    int rc = staged_copy(c, c->d_batch, c->batch_host.data(), (size_t)m * tv * sizeof(float4), c->stream);
-    if (rc != RT_OK) return rc;
+    // new tables go to slots base .. base + nd - 1, never over `prev` if frame 0 reads it
+    const bool keep_prev = dslot[0] == -1;
+    const int base = keep_prev && prev + 1 + nd <= 2 * kBatch ? prev + 1 : 0;
+    for (int j = 0; j < m; ++j) dslot[j] = dslot[j] == -1 ? prev : base + (-2 - dslot[j]);
+    if (nd > 0) {
+      int rc = staged_copy(c, c->d_batch + (size_t)base * tv, c->batch_host.data(), (size_t)nd * tb, c->stream);
+      if (rc != RT_OK) return rc;
+    }
+    // the context's table from here on: the last frame's (host copy first: `last` may point
+    // into batch_host, which the next batch reuses)
+    if (last != c->table.data()) std::memcpy(c->table.data(), last, tb);
     for (int j = 0; j < m; ++j) {
-      c->d_shapes = c->d_batch + (size_t)j * tv;
+      c->d_shapes = c->d_batch + (size_t)dslot[j] * tv;
       c->d_rb = c->d_shapes + rt::rand_table(Sc);
       c->nobj = nobj[j];
       c->nplanes = npl[j];
@@ -1023,14 +1058,10 @@ int rt_compute_frames(rt_ctx* c, float* header, int mode, int frame, int n, uint
       frame = rt_dispatch(c, mode, slot[j]);
       if (frame < 0) return frame;
     }
+    c->batch_last = dslot[m - 1];
   }
-  // leave the context as the per-frame calls would: the last header in its own device copy
+  // the context is left as the per-frame calls would leave it: the last header, its table current
   std::memcpy(c->header.data(), header, bytes);
-  std::memcpy(c->table.data(), c->batch_host.data() + (size_t)((n - 1) % kBatch) * tv, tv * sizeof(float4));
-  int rc = staged_copy(c, c->d_shapes_buf[0], c->table.data(), tv * sizeof(float4), c->stream);
-  if (rc != RT_OK) return rc;
-  c->d_shapes = c->d_shapes_buf[0];
-  c->d_rb = c->d_rb_buf[0];
   return frame;
 }
 
