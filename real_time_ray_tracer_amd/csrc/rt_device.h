@@ -314,13 +314,6 @@ __device__ __forceinline__ int pop_lowest(unsigned long long& m) {
   asm("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(j));
   return j;
 }
-// pop_lowest defined for m == 0 too: s_ff1 returns -1 and m stays 0
-__device__ __forceinline__ int pop_ff1(unsigned long long& m) {
-  int j;
-  asm("s_ff1_i32_b64 %0, %1" : "=s"(j) : "s"(m));
-  asm("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(j));
-  return j;
-}
 
 // One plane of the min-t scan, tested out of index order (after the spheres): plane_eval_ray
 // (p_compute.glsl:111-119) and the scan's acceptance, with the tie rule made explicit.  The

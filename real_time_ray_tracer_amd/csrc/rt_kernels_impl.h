@@ -392,12 +392,6 @@ __device__ __forceinline__ bool bounce_cone_keep_pt(const ConeB& c, float4 g, fl
 #ifndef RT_CLUSTER_TAIL_MAX_G
 #define RT_CLUSTER_TAIL_MAX_G 8
 #endif
-#ifndef RT_B1_RL
-#define RT_B1_RL 0  // first-bounce survivor loop: pre-test rows by v_readlane from the culling lanes
-#endif
-#ifndef RT_B1_PIPE
-#define RT_B1_PIPE 0  // first-bounce survivor loop: the next survivor's pre-test row read ahead
-#endif
 constexpr int kClusterTailMaxG = RT_CLUSTER_TAIL_MAX_G;  // split tail rounds with G <= this use the cluster cull
 __device__ __forceinline__ bool cluster_may_hit(f3 p, f3 d, float4 cb) {
   const float vx = cb.x - p.x, vy = cb.y - p.y, vz = cb.z - p.z;
@@ -1273,10 +1267,10 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           // this loop's per-lane addresses live across the whole pool and spills them to scratch
           const int i = (w << 6) + lane_id_here();
           bool keep;
-          float4 pt = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
           if (pt_ok) {
+            float4 pt;
             keep = i < nobj && bounce_cone_keep_pt(cb, geo[i], pt);
-            if (!RT_B1_RL && i < nobj) geol[i] = pt;
+            if (i < nobj) geol[i] = pt;
           } else {
             keep = i < nobj && !bounce_cone_misses(cb, geo[i]);
           }
@@ -1287,24 +1281,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           exec_tests += (unsigned long long)__popcll(m);
           b1cost += __popcll(m);
           if (ABL == 3) tsec[6] += (unsigned long long)__popcll(m) << 24;  // sections: first-bounce survivors
-          if (pt_ok && RT_B1_RL) {
-            // the pre-test rows stay in the lanes that computed them (lane j: sphere (w << 6) + j)
-            // and survivor j's row is read with v_readlane into scalar registers: no LDS round
-            // trip per survivor, and the split tail rounds' LDS sphere table is not overwritten.
-            // The loop runs with the whole wave (the row of a lane that is not live is read too);
-            // `live` masks the test.
-            const float4* const gw = geo + (w << 6);
-            while (m) {
-              const int j = pop_lowest(m);
-              const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pt.x), j));
-              const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pt.y), j));
-              const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pt.z), j));
-              const float qk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pt.w), j));
-              const bool pass = fmaf(bdir.z, qz, fmaf(bdir.y, qy, bdir.x * qx)) >= qk;
-              if ((__builtin_amdgcn_ballot_w64(pass) & lm1) != 0)
-                sphere_candidate_if(bpos, bdir, gw[j], (w << 6) + j, 0.0001f, t, ind, pass & live);
-            }
-          } else if (pt_ok) {
+          if (pt_ok) {
             geol_valid = false;
             __syncthreads();  // the pre-test rows are written
             if (ABL == 6) lap(5);
@@ -1315,38 +1292,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
             // copies it to a VGPR), and the broadcast read waits at once, as the loop would
             int qbase;
             asm("v_mov_b32 %0, %1" : "=v"(qbase) : "s"((int)(size_t)((const char*)qw - lbase)));
-            if (RT_B1_PIPE && live && m) {
-              // software-pipelined: survivor j's row is requested while survivor j-1 is tested,
-              // so the LDS latency is not paid per survivor (the compiler's waitcnt covers it)
-              auto row = [&](int jj) -> float4 {
-                int a;
-                asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(a) : "s"(jj), "v"(qbase));
-                return *(const float4*)(lbase + a);
-              };
-              // two row buffers in turn (unrolled by 2), so no row is copied between registers
-              // while its read is in flight
-              auto test = [&](const float4& q, int jc) {
-                const bool pass = fmaf(bdir.z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w;
-                if (__builtin_amdgcn_ballot_w64(pass) != 0)
-                  sphere_candidate_if(bpos, bdir, gw[jc], (w << 6) + jc, 0.0001f, t, ind, pass);
-              };
-              int j = pop_ff1(m);
-              float4 qa = row(j), qb;
-              for (;;) {
-                int jc = j;
-                bool more = m != 0;
-                j = pop_ff1(m);  // -1 past the last survivor: the row before qw (in LDS), unused
-                qb = row(j);
-                test(qa, jc);
-                if (!more) break;
-                jc = j;
-                more = m != 0;
-                j = pop_ff1(m);
-                qa = row(j);
-                test(qb, jc);
-                if (!more) break;
-              }
-            } else if (live)
+            if (live)
               while (m) {
                 const int j = pop_lowest(m), k = (w << 6) + j;
                 typedef float v4f __attribute__((ext_vector_type(4)));
