@@ -134,6 +134,16 @@ int rt_compute_frames(rt_ctx* ctx, float* header, int mode, int frame, int n, ui
  * own ring slot, the image is written only by a launch's last frame (the one the caller sees).
  * The ring, the image the caller sees and the header are identical either way. */
 int rt_set_frame_batch(rt_ctx* ctx, int max_frames);
+/* Mode 4 (h_compute) tile schedule, on by default: the 16x16 tiles of a launch are dispatched
+ * longest first, by the bounce rounds their waves needed in recent frames (read back every 16
+ * launches on a side stream; an order is taken up once its upload has landed).  Only the order
+ * of the workgroups changes, never an image.  The dispatch it replaces is the one
+ * glDispatchCompute(WIDTH, HEIGHT, 1) of h_compute (src/main.cpp:604), whose workgroup order
+ * the GL driver chooses.  on = 0 restores row order (and frees the schedule's buffers). */
+int rt_set_tile_schedule(rt_ctx* ctx, int on);
+/* 0 = off, 1 = on with row order still in use (no costs read back yet), 2 = a longest-first
+ * order is in use. */
+int rt_tile_schedule_state(rt_ctx* ctx);
 /* Copy device state to the host in the REFERENCE layout.  Any pointer may be NULL.
  * pixels/normals/depth: [F][W][R] vec4 (x-major, y fastest; R = rows of this context),
  * image: [R][W] rgba32f (row 0 = row_begin, bottom-left origin like the GL texture). */

@@ -57,6 +57,8 @@ SIGNATURES = {
     "rt_dispatch": (C.c_int, [_ctx, C.c_int, C.c_int]),
     "rt_compute_frames": (C.c_int, [_ctx, _fp, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int]),
     "rt_set_frame_batch": (C.c_int, [_ctx, C.c_int]),
+    "rt_set_tile_schedule": (C.c_int, [_ctx, C.c_int]),
+    "rt_tile_schedule_state": (C.c_int, [_ctx]),
     "rt_download": (C.c_int, [_ctx, _fp, _fp, _fp, _fp]),
     "rt_download_rect": (C.c_int, [_ctx, C.c_int, C.c_int, C.c_int, C.c_int, _fp, _fp, _fp, _fp]),
     "rt_upload_gbuffer": (C.c_int, [_ctx, _fp, _fp, _fp]),

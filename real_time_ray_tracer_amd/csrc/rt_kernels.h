@@ -73,6 +73,11 @@ struct FrameParams {
   // multi-frame AO launch (mode 2, gridDim.y = mf_n): frame j reads rand_buffer mf_rb[j * 2 spp ..]
   // and writes slot (mf_slot0 + j) % F (hist_pix / hist_nrm / hist_dep); the image by frame mf_n - 1
   const float4* mf_rb;
+  // hybrid (mode 4) tile schedule (rt_shim hy_schedule): block (x, y) renders the 16x16 tile
+  // tile_order[x + y * gridDim.x] (packed x | y << 16) when non-null, else tile (x, y); each wave
+  // stores its bounce-round count at tile_cost[tile * 4 + wave] when non-null
+  const unsigned* tile_order;
+  unsigned* tile_cost;
 };
 
 // Bounce-ray cluster culling (AO later bounce rounds): at most kMaxClusters clusters (a wave-uniform

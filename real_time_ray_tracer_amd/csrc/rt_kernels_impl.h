@@ -643,7 +643,10 @@ __device__ __forceinline__ void phong_tile(const FrameParams& P, const float4* l
 // sphere table in LDS once ([4][n] + [n] float4), so the culls, the survivors' tests, the shadow
 // rays and the shading read LDS instead of making dependent global round trips, whose latency
 // the few resident waves of these short kernels do not hide.
-constexpr int kTabLdsMax = 128;
+#ifndef RT_TAB_LDS_MAX
+#define RT_TAB_LDS_MAX 128
+#endif
+constexpr int kTabLdsMax = RT_TAB_LDS_MAX;
 __device__ __forceinline__ void stage_tables(const FrameParams& P, float4* lds) {
   const int n = P.nobj;
   stage_shapes(P, lds);
@@ -820,8 +823,10 @@ __device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* 
     if (ABL == 0 || ABL >= 4) lit0 = shadow_lit_cone<PL>(P, geo, n, light, pos + t0 * dir, active && ind0 != -1);  // every lane takes part
     bool live = active && !segment(0, t0, ind0, lit0);
     // segments 1 .. D-1: bounce rounds with the whole wave
+    int rounds = 0;  // wave-uniform: the wave's cost beyond its camera rays (tile schedule)
     for (int seg = 1; seg < (ABL == 5 ? 1 : P.D); ++seg) {
       if (__ballot(live) == 0) break;
+      ++rounds;
       float t;
       int ind;
       bool lit = true;
@@ -836,6 +841,8 @@ __device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* 
       }
       if (live) live = !segment(seg, t, ind, lit);
     }
+    if (P.tile_cost && (threadIdx.x & 63) == 0)  // (a vector store from lane 0)
+      P.tile_cost[((unsigned)by * gridDim.x + (unsigned)bx) * (BWX * BWY) + (threadIdx.x >> 6)] = (unsigned)rounds;
   } else {
     for (int seg = 0; active && seg < P.D; ++seg) {  // helper depth D, D-1, ..., 1
       float t;
@@ -872,7 +879,17 @@ __global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(FrameParams P) {
       hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x,
                                                  blockIdx.y * kHybridTilesPerBlock + t, frame_dst(P, blockIdx.z));
   } else if constexpr (kHybridFramesPerBlock == 1) {  // no frame loop (the loop form costs 3-4% at (b))
-    hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x, blockIdx.y,
+    // the host's tile schedule (longest first, from the previous frames' bounce rounds): the
+    // few tiles whose mirror paths bounce for many rounds start early instead of setting the
+    // launch's tail (config (b): 32.0 -> 25.4 us per frame with the reverse of row order, which
+    // happens to put that scene's bouncing tiles first)
+    unsigned bx = blockIdx.x, by = blockIdx.y;
+    if (P.tile_order) {
+      const unsigned t = P.tile_order[blockIdx.x + blockIdx.y * gridDim.x];
+      bx = t & 0xffffu;
+      by = t >> 16;
+    }
+    hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), bx, by,
                                                frame_dst(P, blockIdx.z));
   } else {
     int j0;

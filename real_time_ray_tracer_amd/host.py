@@ -253,6 +253,14 @@ class Renderer:
         by each launch's last frame (rt_set_frame_batch)."""
         self._c(self._lib.rt_set_frame_batch(self.ctx, int(max_frames)), "rt_set_frame_batch")
 
+    def set_tile_schedule(self, on: bool):
+        """Mode 4's longest-first tile order (rt_set_tile_schedule; on by default)."""
+        self._c(self._lib.rt_set_tile_schedule(self.ctx, int(bool(on))), "rt_set_tile_schedule")
+
+    def tile_schedule_state(self) -> int:
+        """0 off, 1 on (row order so far), 2 a longest-first order in use (rt_tile_schedule_state)."""
+        return self._c(self._lib.rt_tile_schedule_state(self.ctx), "rt_tile_schedule_state")
+
     def download(self, pixels=True, normals=True, depth=True, image=True) -> GBuffer:
         shp = (self.F, self.W, self.R, 4)
         p = np.empty(shp, np.float32) if pixels else None
