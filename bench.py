@@ -323,6 +323,8 @@ def main():
                          "writes the image) are timed instead; either way the other shape is reported beside it")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N>1 path with ranks sharing GPUs, gather staged through host")
+    ap.add_argument("--no-tile-schedule", action="store_true",
+                    help="workgroups in the plain order (rt_set_tile_schedule(0)) instead of longest first")
     ap.add_argument("--no-alt-dispatch", action="store_true",
                     help="modes 2-4: skip timing the other dispatch shape (counter runs: every dispatch then has "
                          "the timed shape, so per-dispatch counters are per frame)")
@@ -457,6 +459,8 @@ def main():
     rend = Renderer(W, H, S, spp, device=gpu, rows=(r0, r1))
     if args.frame_batch > 0:
         rend.set_frame_batch(args.frame_batch)
+    if args.no_tile_schedule:
+        rend.set_tile_schedule(False)
     rend.set_stream(stream)
     # pipelined mode 1: post-process (and the image consumers: the gather) on a second stream
     pipeline = mode == 1 and not args.no_pipeline
@@ -818,6 +822,9 @@ def main():
             "host_enqueue_ms_per_step": round(max(0.0, host_s * 1e3 - host_wait_ms) / args.steps, 4),
             "host_backpressure_ms_per_step": round(host_wait_ms / args.steps, 4),
             "build": binfo,
+            "tile_schedule": ("off: workgroups in the plain order" if args.no_tile_schedule else
+                              "longest first (rt_set_tile_schedule: mode-4 tiles by the bounce rounds of recent "
+                              "frames; state %d)" % rend.tile_schedule_state()),
         }
         if host_loop and mode in (2, 3, 4):
             out["dispatch"] = (("one launch and one image write per frame (rt_set_frame_batch(1)): the reference's "

@@ -55,29 +55,31 @@ struct Stage {
   bool used = false;
 };
 
-// Tile schedule of the hybrid kernel (mode 4): a launch's time is its longest waves' (the few
-// tiles whose mirror paths bounce for many rounds), so the tiles go longest first.  The waves
-// record their bounce rounds (d_cost); every kHyPeriod-th launch the costs are read back on a
-// side stream, and when the sorted order changes it is uploaded into the table no launch in
-// flight reads, which becomes the active one once the copy has landed.  Nothing here waits on
-// the GPU or puts a copy between two launches on the main stream; the permutation only moves
-// tiles between blocks, so the images do not depend on it.
-struct HySched {
-  int gx = 0, gy = 0, ntiles = 0;
-  unsigned* d_cost = nullptr;          // [ntiles * 4]
-  unsigned* d_order[2] = {};           // [ntiles] each: packed x | y << 16
+// Longest-first workgroup schedule.  A launch's time is set by its longest workgroups when they
+// start late: the few hybrid tiles (mode 4) whose mirror paths bounce for many rounds.  The waves
+// record their bounce rounds in d_cost; every kSchedPeriod-th launch the costs are read back on
+// a side stream, and when the sorted order changes it is uploaded into the table no launch in
+// flight reads, which becomes the active one once the copy has landed.  Nothing here waits on the GPU or puts a copy between two launches
+// on a launch stream; the permutation only moves work between workgroups, so the images do not
+// depend on it.
+enum { kSchedHybrid = 0, kSchedKinds = 1 };
+struct TileSched {
+  int gx = 0, gy = 0, nunits = 0, per_unit = 1;  // units (tiles / pools) = gx * gy; cost slots per unit
+  unsigned* d_cost = nullptr;          // [nunits * per_unit]
+  unsigned* d_order[2] = {};           // [nunits] each
   unsigned* h_cost = nullptr;          // pinned
   unsigned* h_order[2] = {};           // pinned
   hipStream_t side = nullptr;
-  hipEvent_t ev_launch = nullptr, ev_cost = nullptr, ev_order = nullptr, ev_use[2] = {};
-  bool use_recorded[2] = {};
-  int active = -1;                     // the table launches read (-1: row-major order)
+  hipEvent_t ev_launch = nullptr, ev_cost = nullptr, ev_order = nullptr;
+  hipEvent_t ev_use[2][3] = {};        // per table: its last readers on each launch stream
+  hipStream_t used_on[2][3] = {};      // the launch streams a table was read on
+  int active = -1;                     // the table launches read (-1: the plain order)
   int pending = -1;                    // the table being uploaded
   bool cost_inflight = false;
   long long launches = 0;
   std::vector<unsigned> cur, next;     // the active / pending order
 };
-constexpr int kHyPeriod = 16;
+constexpr int kSchedPeriod = 16;
 
 }  // namespace
 
@@ -119,8 +121,8 @@ struct rt_ctx {
   float4* d_xfer = nullptr;    // rt_download / rt_upload_gbuffer: one array in the reference layout [F][W][R]
   float4* d_batch = nullptr;   // rt_compute_frames: device table copies, 2 x kBatch slots (one per distinct table)
   int batch_last = -1;         // the d_batch slot d_shapes points into after rt_compute_frames (else -1)
-  HySched hy;                  // hybrid tile schedule (lazily set up by the first mode-4 launch)
-  bool hy_sched_on = true;     // rt_set_tile_schedule
+  TileSched sched[kSchedKinds];  // longest-first schedules (set up by the first launch of each kind)
+  bool sched_on = true;          // rt_set_tile_schedule
   float4* d_mf_rb = nullptr;   // rt_compute_frames, mode 2: the rand_buffers of a multi-frame launch
   std::vector<float4> batch_host;
   std::vector<float> batch_hdr;  // the batch's host headers (camera, light: launch parameters)
@@ -212,23 +214,24 @@ int staged_copy(rt_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t
   return RT_OK;
 }
 
-void free_hy(HySched& h) {
+void free_sched(TileSched& h) {
   if (h.side) (void)hipStreamSynchronize(h.side);
   if (h.d_cost) (void)hipFree(h.d_cost);
   for (int k = 0; k < 2; ++k) {
     if (h.d_order[k]) (void)hipFree(h.d_order[k]);
     if (h.h_order[k]) (void)hipHostFree(h.h_order[k]);
-    if (h.ev_use[k]) (void)hipEventDestroy(h.ev_use[k]);
+    for (auto e : h.ev_use[k])
+      if (e) (void)hipEventDestroy(e);
   }
   if (h.h_cost) (void)hipHostFree(h.h_cost);
   for (auto e : {h.ev_launch, h.ev_cost, h.ev_order})
     if (e) (void)hipEventDestroy(e);
   if (h.side) (void)hipStreamDestroy(h.side);
-  h = HySched{};
+  h = TileSched{};
 }
 
 void free_all(rt_ctx* c) {
-  free_hy(c->hy);
+  for (auto& h : c->sched) free_sched(h);
   for (auto& s : c->stage) {
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.host) (void)hipHostFree(s.host);
@@ -363,26 +366,30 @@ int launch(rt_ctx* c, int program, const rt::FrameParams& p, hipStream_t st) {
 }
 int launch(rt_ctx* c, int program, const rt::FrameParams& p) { return launch(c, program, p, c->stream); }
 
-// Before a hybrid launch: take up a landed order table, turn landed costs into an order, and
-// set the launch's tile_order / tile_cost (see HySched).
-int hy_before(rt_ctx* c, rt::FrameParams& p) {
-  HySched& h = c->hy;
-  if (!c->hy_sched_on) return RT_OK;
-  const int gx = (p.W + 15) / 16, gy = (p.trace_rows + 15) / 16;
-  if (h.ntiles && (h.gx != gx || h.gy != gy)) free_hy(h);
-  if (!h.ntiles) {
+// Before a launch of schedule `kind` over gx x gy units (cost slots per_unit each): take up a
+// landed order table, turn landed costs into an order, and set the launch's tile_order /
+// tile_cost (see TileSched).
+int sched_before(rt_ctx* c, int kind, int gx, int gy, int per_unit, rt::FrameParams& p) {
+  TileSched& h = c->sched[kind];
+  if (!c->sched_on || gx < 1 || gy < 1) return RT_OK;
+  if (h.nunits && (h.gx != gx || h.gy != gy || h.per_unit != per_unit)) {
+    RT_HIP(c, hipDeviceSynchronize());  // (never in practice: a context's launch shapes are fixed)
+    free_sched(h);
+  }
+  if (!h.nunits) {
     if (gx >= 65536 || gy >= 65536) return RT_OK;
     h.gx = gx;
     h.gy = gy;
-    h.ntiles = gx * gy;
-    const size_t nc = (size_t)h.ntiles * 4 * sizeof(unsigned), no = (size_t)h.ntiles * sizeof(unsigned);
+    h.per_unit = per_unit;
+    h.nunits = gx * gy;
+    const size_t nc = (size_t)h.nunits * per_unit * sizeof(unsigned), no = (size_t)h.nunits * sizeof(unsigned);
     RT_HIP(c, hipMalloc(&h.d_cost, nc));
     RT_HIP(c, hipMemsetAsync(h.d_cost, 0, nc, c->stream));
     RT_HIP(c, hipHostMalloc(&h.h_cost, nc, hipHostMallocDefault));
     for (int k = 0; k < 2; ++k) {
       RT_HIP(c, hipMalloc(&h.d_order[k], no));
       RT_HIP(c, hipHostMalloc(&h.h_order[k], no, hipHostMallocDefault));
-      RT_HIP(c, hipEventCreateWithFlags(&h.ev_use[k], hipEventDisableTiming));
+      for (auto& e : h.ev_use[k]) RT_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     RT_HIP(c, hipStreamCreateWithFlags(&h.side, hipStreamNonBlocking));
     RT_HIP(c, hipEventCreateWithFlags(&h.ev_launch, hipEventDisableTiming));
@@ -396,30 +403,34 @@ int hy_before(rt_ctx* c, rt::FrameParams& p) {
     return q == hipSuccess;
   };
   if (h.pending >= 0 && landed(h.ev_order)) {
-    if (h.active >= 0) {  // the launches enqueued so far are the old table's last readers
-      RT_HIP(c, hipEventRecord(h.ev_use[h.active], c->stream));
-      h.use_recorded[h.active] = true;
-    }
+    if (h.active >= 0)  // the launches enqueued so far are the old table's last readers
+      for (int s = 0; s < 3; ++s)
+        if (h.used_on[h.active][s]) RT_HIP(c, hipEventRecord(h.ev_use[h.active][s], h.used_on[h.active][s]));
     h.active = h.pending;
     h.pending = -1;
     h.cur.swap(h.next);
+    for (auto& st : h.used_on[h.active]) st = nullptr;
   }
   if (h.cost_inflight && landed(h.ev_cost)) {
     h.cost_inflight = false;
     if (h.pending < 0) {
-      // longest first: a tile's cost is its slowest wave's bounce rounds; ties keep row order
-      std::vector<unsigned> cost(h.ntiles);
-      for (int t = 0; t < h.ntiles; ++t)
-        cost[t] = std::max(std::max(h.h_cost[4 * t], h.h_cost[4 * t + 1]), std::max(h.h_cost[4 * t + 2], h.h_cost[4 * t + 3]));
-      std::vector<unsigned> idx(h.ntiles);
-      for (int t = 0; t < h.ntiles; ++t) idx[t] = (unsigned)t;
+      // longest first: a unit's cost is its slowest slot's; ties keep the plain order
+      std::vector<unsigned> cost(h.nunits);
+      for (int t = 0; t < h.nunits; ++t) {
+        unsigned v = 0;
+        for (int k = 0; k < h.per_unit; ++k) v = std::max(v, h.h_cost[(size_t)t * h.per_unit + k]);
+        cost[t] = v;
+      }
+      std::vector<unsigned> idx(h.nunits);
+      for (int t = 0; t < h.nunits; ++t) idx[t] = (unsigned)t;
       std::stable_sort(idx.begin(), idx.end(), [&](unsigned a, unsigned b) { return cost[a] > cost[b]; });
-      for (auto& t : idx) t = (t % (unsigned)h.gx) | ((t / (unsigned)h.gx) << 16);
+      for (auto& t : idx) t = (t % (unsigned)h.gx) | ((t / (unsigned)h.gx) << 16);  // packed x | y << 16
       const bool uniform = std::all_of(cost.begin(), cost.end(), [&](unsigned v) { return v == cost[0]; });
       if (!uniform && idx != h.cur) {
         const int x = h.active == 0 ? 1 : 0;  // the table no launch reads from now on
         std::memcpy(h.h_order[x], idx.data(), idx.size() * sizeof(unsigned));
-        if (h.use_recorded[x]) RT_HIP(c, hipStreamWaitEvent(h.side, h.ev_use[x], 0));
+        for (int s = 0; s < 3; ++s)
+          if (h.used_on[x][s]) RT_HIP(c, hipStreamWaitEvent(h.side, h.ev_use[x][s], 0));
         RT_HIP(c, hipMemcpyAsync(h.d_order[x], h.h_order[x], idx.size() * sizeof(unsigned), hipMemcpyHostToDevice,
                                  h.side));
         RT_HIP(c, hipEventRecord(h.ev_order, h.side));
@@ -433,20 +444,49 @@ int hy_before(rt_ctx* c, rt::FrameParams& p) {
   return RT_OK;
 }
 
-// After a hybrid launch on `st`: every kHyPeriod-th one has its costs read back on the side stream
-// (the launches after it may overwrite them meanwhile: a cost is a hint, never a result).
-int hy_after(rt_ctx* c, hipStream_t st) {
-  HySched& h = c->hy;
-  if (!c->hy_sched_on || !h.ntiles) return RT_OK;
-  if (h.launches++ % kHyPeriod == 0 && !h.cost_inflight) {
+// After a launch of schedule `kind` on stream `st`: note that the active table was read on st;
+// every kSchedPeriod-th launch has its costs read back on the side stream (launches after it may
+// overwrite them meanwhile: a cost is a hint, never a result).
+int sched_after(rt_ctx* c, int kind, hipStream_t st) {
+  TileSched& h = c->sched[kind];
+  if (!c->sched_on || !h.nunits) return RT_OK;
+  if (h.active >= 0) {
+    hipStream_t* u = h.used_on[h.active];
+    for (int s = 0; s < 3; ++s) {
+      if (u[s] == st) break;
+      if (!u[s]) {
+        u[s] = st;
+        break;
+      }
+    }
+  }
+  if (h.launches++ % kSchedPeriod == 0 && !h.cost_inflight) {
     RT_HIP(c, hipEventRecord(h.ev_launch, st));
     RT_HIP(c, hipStreamWaitEvent(h.side, h.ev_launch, 0));
-    RT_HIP(c, hipMemcpyAsync(h.h_cost, h.d_cost, (size_t)h.ntiles * 4 * sizeof(unsigned), hipMemcpyDeviceToHost,
-                             h.side));
+    RT_HIP(c, hipMemcpyAsync(h.h_cost, h.d_cost, (size_t)h.nunits * h.per_unit * sizeof(unsigned),
+                             hipMemcpyDeviceToHost, h.side));
     RT_HIP(c, hipEventRecord(h.ev_cost, h.side));
     h.cost_inflight = true;
   }
   return RT_OK;
+}
+
+// A launch of `program` with its schedule (hybrid tiles, AO pools), if it has one.
+int launch_sched(rt_ctx* c, int program, rt::FrameParams& p, hipStream_t st) {
+  int kind = -1, gx = 0, gy = 1, per = 1;
+  if (program == RT_PROG_H_COMPUTE) {
+    kind = kSchedHybrid;
+    gx = (p.W + 15) / 16;
+    gy = (p.trace_rows + 15) / 16;
+    per = 4;
+  }
+  // (AO pools in the same longest-first order by wave time measured nothing at (c) and (d): those
+  // launches are not tail-bound; the kernel's bookkeeping cost registers, profiles/r04h_*)
+  if (kind < 0) return launch(c, program, p, st);
+  int rc = sched_before(c, kind, gx, gy, per, p);
+  if (rc == RT_OK) rc = launch(c, program, p, st);
+  if (rc == RT_OK) rc = sched_after(c, kind, st);
+  return rc;
 }
 
 int run_program(rt_ctx* c, int program, int frame) {
@@ -464,13 +504,7 @@ int run_program(rt_ctx* c, int program, int frame) {
       p.trace_row0 = c->own0;
       p.trace_rows = c->own_rows;
       p.out_pix = c->pix[c->pix_slot[frame]];
-      if (program == RT_PROG_H_COMPUTE) {
-        int rc = hy_before(c, p);
-        if (rc == RT_OK) rc = launch(c, program, p);
-        if (rc == RT_OK) rc = hy_after(c, c->stream);
-        return rc;
-      }
-      return launch(c, program, p);
+      return launch_sched(c, program, p, c->stream);
     case RT_PROG_AO_COMPUTE:
     case RT_PROG_AOP_COMPUTE:
       // g-buffer writers trace the halo rows too, so a strip's ring evolves exactly like the
@@ -519,13 +553,7 @@ int run_program_mf(rt_ctx* c, int program, int slot0, int m, const float4* light
   if (ao) p.mf_rb = c->d_mf_rb;
   else
     for (int j = 0; j < m; ++j) p.mf_light[j] = lights[j];
-  if (program == RT_PROG_H_COMPUTE) {
-    int rc = hy_before(c, p);
-    if (rc == RT_OK) rc = launch(c, program, p);
-    if (rc == RT_OK) rc = hy_after(c, c->stream);
-    return rc;
-  }
-  return launch(c, program, p);
+  return launch_sched(c, program, p, c->stream);
 }
 
 // One pipelined mode-1 frame (see the header comment): AO on the frame's AO stream into free
@@ -1209,14 +1237,17 @@ int rt_set_tile_schedule(rt_ctx* c, int on) {
   if (!c) return RT_E_INVAL;
   RT_HIP(c, hipSetDevice(c->device));
   RT_HIP(c, hipStreamSynchronize(c->stream));  // no launch in flight reads the tables freed here
-  free_hy(c->hy);
-  c->hy_sched_on = on != 0;
+  for (auto& h : c->sched) free_sched(h);
+  c->sched_on = on != 0;
   return RT_OK;
 }
 
 int rt_tile_schedule_state(rt_ctx* c) {
   if (!c) return RT_E_INVAL;
-  return c->hy_sched_on ? (c->hy.active >= 0 ? 2 : 1) : 0;
+  if (!c->sched_on) return 0;
+  for (auto& h : c->sched)
+    if (h.active >= 0) return 2;
+  return 1;
 }
 
 int rt_set_frame_batch(rt_ctx* c, int max_frames) {

@@ -75,3 +75,4 @@ def test_tile_schedule_off_and_on_again():
     r.synchronize()
     assert r.tile_schedule_state() in (1, 2)
     r.close()
+
