@@ -300,7 +300,9 @@ def load_traffic(cfg_name: str, src_sha1):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed frames (default 20; configs (a) and (b), whose frames are 7-26 us, 1000 and 400 "
+                         "so the timed region is >= 7 ms)")
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", default="d", choices=sorted(CONFIGS))
     ap.add_argument("--no-balance", action="store_true", help="equal strips instead of cost-balanced")
@@ -334,6 +336,8 @@ def main():
     ap.add_argument("--inject-failure", type=int, default=-1, metavar="RANK",
                     help="test hook: this rank raises right after the process group is up")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = {"a": 1000, "b": 400}.get(args.config, 20)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
