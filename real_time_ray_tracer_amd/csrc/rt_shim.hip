@@ -792,6 +792,9 @@ int rt_set_stream(rt_ctx* c, void* s) {
   for (auto& r : c->post_recorded) r = false;
   c->pipe_n = 0;
   c->img_stream = nullptr;  // everything is finished (sync_all above)
+  for (auto& h : c->sched)  // no launch reads an order table any more: forget the old streams
+    for (auto& u : h.used_on)
+      for (auto& st : u) st = nullptr;
   c->stream = (hipStream_t)s;  // NULL = the legacy NULL stream
   if (!c->pipelined) c->out_stream = c->stream;
   // an idle own stream is released: every stream holds one of the process's few hardware
