@@ -1677,28 +1677,22 @@ __device__ __forceinline__ void xcd_tile(unsigned R, unsigned& bx, unsigned& by)
 #ifndef RT_POST_BWY
 #define RT_POST_BWY 4
 #endif
-#ifndef RT_POST_ROWS
-#define RT_POST_ROWS 1  // block rows per block, one after another (A/B builds)
-#endif
 constexpr int kPostWX = RT_POST_WX, kPostWY = 64 / RT_POST_WX, kPostBWX = RT_POST_BWX, kPostBWY = RT_POST_BWY;
-constexpr int kPostTileW = kPostWX * kPostBWX, kPostTileH = kPostWY * kPostBWY, kPostRows = RT_POST_ROWS;
+constexpr int kPostTileW = kPostWX * kPostBWX, kPostTileH = kPostWY * kPostBWY;
 static_assert(kPostWX * kPostWY == 64 && kPostBWX * kPostBWY * 64 == kBlock, "post tile shape");
 
 __global__ __launch_bounds__(kBlock) void post_kernel(FrameParams P) {
-  int x, y0;
+  int x, y;
   unsigned bx, by;
   xcd_tile((unsigned)P.tile_run, bx, by);
   {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     x = (int)bx * kPostTileW + (wave % kPostBWX) * kPostWX + lane % kPostWX;
-    y0 = P.trace_row0 + (int)by * kPostTileH * kPostRows + (wave / kPostBWX) * kPostWY + lane / kPostWX;
+    y = P.trace_row0 + (int)by * kPostTileH + (wave / kPostBWX) * kPostWY + lane / kPostWX;
   }
+  const bool active = x < P.W && y < P.trace_row0 + P.trace_rows;
   unsigned filtered = 0, visited = 0, accepted = 0;
-#pragma unroll 1
-  for (int r = 0; r < kPostRows; ++r) {
-    const int y = y0 + r * kPostTileH;
-    if (x < P.W && y < P.trace_row0 + P.trace_rows) post_pixel(P, x, y, filtered, visited, accepted);
-  }
+  if (active) post_pixel(P, x, y, filtered, visited, accepted);
   if (P.counters) {
     unsigned n = wave_sum(filtered), v = wave_sum(visited), a = wave_sum(accepted);
     if ((threadIdx.x & 63) == 0) {
@@ -1736,7 +1730,7 @@ __device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, u
   float4 color = P.raw[off];
   const size_t np = dep_plane(P);  // normals: xyz plane + w plane (nrm_store)
   if (nrm_load_w(P.nrm, np, off) > 0.99f) {
-    ++filtered;
+    filtered = 1;
     // Memory round trips, not bytes, are what this kernel costs in the pipelined frame: there it
     // runs beside the next frame's AO pass, and each resident post-process wave holds registers
     // an AO wave could use for as long as it waits on memory.  So the neighbours are requested in
@@ -2039,8 +2033,7 @@ inline hipError_t launch_production(int program, const FrameParams& p, const Fra
       break;
     case K_POST:
       hipLaunchKernelGGL(post_kernel,
-                         dim3((p.W + kPostTileW - 1) / kPostTileW,
-                              (p.trace_rows + kPostTileH * kPostRows - 1) / (kPostTileH * kPostRows)),
+                         dim3((p.W + kPostTileW - 1) / kPostTileW, (p.trace_rows + kPostTileH - 1) / kPostTileH),
                          dim3(kBlock), 0, stream, q);
       break;
     default:
