@@ -29,6 +29,7 @@ struct FrameParams {
   int b1_min;                // AO: least live lanes of a prepared batch for its batched first bounce (set at launch)
   int pool_rot;              // AO: pools per rotation group (one row's; 0 = pools in row order; set at launch)
   int tile_run;              // post-process: tiles per XCD run (xcd_tile; set at launch)
+  int post_sx, post_sy;      // post-process: super-tiles of post_sx x post_sy blocks per XCD visit (xcd_tile)
   float inv_spp, fW, fH;     // 1.0f / spp, (float)W, (float)H: host-computed wave-uniform constants
   float inv_W, inv_H;        // 1.0f / fW, 1.0f / fH (correctly rounded; div_rn_by)
   float hx, hy, hz;          // horizontal

@@ -1649,7 +1649,32 @@ __device__ __forceinline__ void post_pixel(const FrameParams& P, int x, int y, u
 // per XCD cut the bytes by 19% but made the launch 43% slower; runs of 1/8 row, 11% slower).
 // L -> run (L / 8 / R) * 8 + L mod 8, offset (L / 8) mod R: a bijection on the first multiple
 // of 8R tiles; the rest keep their order.
-__device__ __forceinline__ void xcd_tile(unsigned R, unsigned& bx, unsigned& by) {
+//
+// Round 4: when the host finds super-tiles of SX x SY blocks that tile the grid (launch_params:
+// SX, SY in {4, 2} dividing gx, gy), each XCD takes whole super-tiles, dealt round-robin (row-major
+// blocks inside), so a block's upper and lower neighbour rows are mostly in its own L2 too:
+// config (d) post-process PMC 1.085 -> 1.044x the byte model, per-launch and pipelined-frame
+// times unchanged (profiles/r04o_ab_post_super_tiles.txt; 4 x 12: 1.035x, 2 x 6: 1.052x).
+// L -> super-tile (L / 8 / SS) * 8 + L mod 8, block (L / 8) mod SS for the first multiple of 8
+// super-tiles; the rest in order: a bijection.
+__device__ __forceinline__ void xcd_tile(unsigned R, unsigned SX, unsigned SY, unsigned& bx, unsigned& by) {
+  if (SX * SY > 1) {
+    const unsigned gx = gridDim.x, L = blockIdx.x + blockIdx.y * gx, SS = SX * SY;
+    const unsigned gsx = gx / SX, Q = gsx * (gridDim.y / SY), M = Q / 8 * 8;
+    unsigned q, o;
+    if (L < M * SS) {
+      const unsigned j = L >> 3;
+      q = (j / SS) * 8 + (L & 7u);
+      o = j % SS;
+    } else {
+      const unsigned L2 = L - M * SS;
+      q = M + L2 / SS;
+      o = L2 % SS;
+    }
+    bx = (q % gsx) * SX + o % SX;
+    by = (q / gsx) * SY + o / SX;
+    return;
+  }
   const unsigned gx = gridDim.x, n = gx * gridDim.y, L = blockIdx.x + blockIdx.y * gx;
   const unsigned M = R ? n / (8 * R) * (8 * R) : 0;
   unsigned t = L;
@@ -1684,7 +1709,7 @@ static_assert(kPostWX * kPostWY == 64 && kPostBWX * kPostBWY * 64 == kBlock, "po
 __global__ __launch_bounds__(kBlock) void post_kernel(FrameParams P) {
   int x, y;
   unsigned bx, by;
-  xcd_tile((unsigned)P.tile_run, bx, by);
+  xcd_tile((unsigned)P.tile_run, (unsigned)P.post_sx, (unsigned)P.post_sy, bx, by);
   {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     x = (int)bx * kPostTileW + (wave % kPostBWX) * kPostWX + lane % kPostWX;
@@ -1975,6 +2000,11 @@ inline FrameParams launch_params(const FrameParams& p) {
 #ifdef RT_POST_RUN
     q.tile_run = RT_POST_RUN;  // A/B builds: a fixed run length (0 = row-major order)
 #endif
+    // super-tiles (xcd_tile): 4 or 2 blocks each way where that divides the grid
+    const int gy = (p.trace_rows + kPostTileH - 1) / kPostTileH;
+    q.post_sx = gx % 4 == 0 ? 4 : (gx % 2 == 0 ? 2 : 1);
+    q.post_sy = gy % 4 == 0 ? 4 : (gy % 2 == 0 ? 2 : 1);
+    if (gx < 8 * q.post_sx) q.post_sx = q.post_sy = 1;  // narrow frames: the runs (or none)
   }
   return q;
 }
