@@ -325,6 +325,8 @@ def main():
                          "writes the image) are timed instead; either way the other shape is reported beside it")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N>1 path with ranks sharing GPUs, gather staged through host")
+    ap.add_argument("--out-stream-priority", type=int, default=0,
+                    help="mode 1 pipelined: torch priority of the post-process (output) stream (lower = higher)")
     ap.add_argument("--no-tile-schedule", action="store_true",
                     help="workgroups in the plain order (rt_set_tile_schedule(0)) instead of longest first")
     ap.add_argument("--no-alt-dispatch", action="store_true",
@@ -468,7 +470,7 @@ def main():
     rend.set_stream(stream)
     # pipelined mode 1: post-process (and the image consumers: the gather) on a second stream
     pipeline = mode == 1 and not args.no_pipeline
-    out_stream = torch.cuda.Stream(dev) if pipeline else stream
+    out_stream = torch.cuda.Stream(dev, priority=args.out_stream_priority) if pipeline else stream
     if pipeline:
         rend.enable_pipelining(True, out_stream)
     streams = {"out": out_stream}
