@@ -76,3 +76,35 @@ def test_tile_schedule_off_and_on_again():
     assert r.tile_schedule_state() in (1, 2)
     r.close()
 
+
+
+def test_tile_schedule_survives_a_stream_change():
+    """rt_set_stream after the order is in use (the context's own stream is released): later
+    frames, with the schedule still engaged, equal the same frames rendered in row order."""
+    import torch
+
+    W, H, S, spp, mode, _ = CONFIGS["b"]
+
+    def run(schedule):
+        h = config_header("b")
+        r = Renderer(W, H, S, spp)
+        r.set_tile_schedule(schedule)
+        f = 0
+        for k in range(60):
+            if k == 30:
+                r.synchronize()
+                st = torch.cuda.Stream()
+                r.set_stream(st)
+            h.moving_light(True)
+            h.set_mode(f, h.num_objects)
+            r.upload_header(h)
+            f = r.dispatch(mode, f)
+        r.synchronize()
+        img, state = r.image(), r.tile_schedule_state()
+        r.close()
+        return img, state
+
+    img, state = run(True)
+    img2, state2 = run(False)
+    assert state == 2 and state2 == 0
+    assert np.array_equal(img.view(np.uint32), img2.view(np.uint32))
