@@ -61,12 +61,12 @@ variant:
 
 $(ORACLE): oracle/rt_oracle.c oracle/rt_oracle.h include/rt/layout.h
 	@mkdir -p oracle/build
-	$(CC) $(CFLAGS_ORACLE) -shared -o $@ oracle/rt_oracle.c -lm
+	$(CC) $(CFLAGS_ORACLE) -shared -o $@ oracle/rt_oracle.c -lquadmath -lm
 
 # CPU-baseline build for the GPU box's AMD EPYC (Zen 5) host cores; same source and float flags
 $(ORACLE_NATIVE): oracle/rt_oracle.c oracle/rt_oracle.h include/rt/layout.h
 	@mkdir -p oracle/build
-	$(CC) $(subst -march=x86-64-v3,-march=znver3 -mtune=znver3 -mavx512f -mavx512cd -mavx512bw -mavx512dq -mavx512vl,$(CFLAGS_ORACLE)) -shared -o $@ oracle/rt_oracle.c -lm
+	$(CC) $(subst -march=x86-64-v3,-march=znver3 -mtune=znver3 -mavx512f -mavx512cd -mavx512bw -mavx512dq -mavx512vl,$(CFLAGS_ORACLE)) -shared -o $@ oracle/rt_oracle.c -lquadmath -lm
 
 $(HEADLESS): $(CSRC)/rt_headless.cpp $(LIB) include/rt/*.h
 	$(CXX) -O2 -std=c++17 -Iinclude -o $@ $< -L$(PKG) -lrtrt -Wl,-rpath,'$$ORIGIN/../$(PKG)'

@@ -12,6 +12,10 @@ N GPUs split the SAME frame into cost-balanced row strips (strong scaling).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config b|c|d|e]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+--gpus N means N ranks.  Without a launcher (WORLD_SIZE unset) and N > 1, bench.py starts
+torch.distributed.run with N processes on 127.0.0.1 itself, before anything touches the GPU, and
+exits with its status; under a launcher, WORLD_SIZE must equal N or the run exits non-zero.
+
 Rank 0 prints one JSON line.  Mrays/s = W*H*spp*K / time (primary samples, whole job).
 """
 from __future__ import annotations
@@ -297,6 +301,64 @@ def load_traffic(cfg_name: str, src_sha1):
     return found[0] if found else (None, None)
 
 
+def rank_devices(world, rank, gpu, cdev):
+    """every rank's (device index, PCI bus) on every rank: a world x 2 all-reduce"""
+    import torch
+    import torch.distributed as dist
+
+    props = torch.cuda.get_device_properties(gpu)
+    t = torch.zeros(world, 2, dtype=torch.float64, device=cdev)
+    t[rank, 0] = gpu
+    t[rank, 1] = getattr(props, "pci_bus_id", -1)
+    if world > 1:
+        dist.all_reduce(t)
+    return [{"device": int(t[i, 0].item()), "pci_bus": int(t[i, 1].item())} for i in range(world)]
+
+
+def launch_report(args, world, rank, local_rank):
+    """--launch-check: the ranks are up and agree; rank 0 reports who runs where"""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.zeros(world, 3, dtype=torch.float64)
+    t[rank] = torch.tensor([local_rank, os.getpid(), 1.0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "gpus_arg": args.gpus, "backend": args.backend,
+                          "launched_by": os.environ.get("RTRT_BENCH_LAUNCHER", "external launcher"),
+                          "ranks": [{"rank": i, "local_rank": int(t[i, 0].item()), "pid": int(t[i, 1].item())}
+                                    for i in range(world)],
+                          "ranks_up": int(t[:, 2].sum().item())}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def launch_ranks(argv) -> int:
+    """--gpus N > 1 without a launcher: run this script as N ranks under torch.distributed.run
+    (one process per GPU, 127.0.0.1 rendezvous on a free port) and return its exit status.  Called
+    before anything initialises HIP in this process (nothing here touches the GPU), so the ranks
+    are children of a clean parent; the parent never execs."""
+    import socket
+    import subprocess
+
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    n = ap.parse_known_args(argv)[0].gpus
+    if n <= 1 or "WORLD_SIZE" in os.environ:
+        return -1
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, RTRT_BENCH_LAUNCHER=f"bench.py --gpus {n}: torch.distributed.run, {n} ranks")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + list(argv)
+    print(f"bench.py: starting {n} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -337,6 +399,9 @@ def main():
                          "takes the others down within this time instead of hanging the job)")
     ap.add_argument("--inject-failure", type=int, default=-1, metavar="RANK",
                     help="test hook: this rank raises right after the process group is up")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="stop after the start-up check: rank 0 prints one JSON line with the world size and each "
+                         "rank's device (the N-rank launch without a frame; runs on the CPU with --backend gloo)")
     args = ap.parse_args()
     if args.steps is None:
         args.steps = {"a": 1000, "b": 400}.get(args.config, 20)
@@ -344,6 +409,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:  # (launch_ranks starts the ranks when no launcher did)
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: a run asked for N GPUs must run N ranks")
     import torch
     import torch.distributed as dist
 
@@ -370,10 +437,13 @@ def main():
         dist.all_reduce(chk)
         if int(chk[0].item()) != world or int(chk[1].item()) != world * args.steps:
             raise RuntimeError(f"ranks disagree at start-up: {chk.tolist()} (world {world}, steps {args.steps})")
+    if args.launch_check:
+        return launch_report(args, world, rank, local_rank)
     gpu = local_rank if args.backend == "nccl" else local_rank % torch.cuda.device_count()
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     cdev = dev if args.backend == "nccl" else torch.device("cpu")  # collective tensors
+    devices = rank_devices(world, rank, gpu, cdev)
 
     W, H, S, spp, mode, desc = CONFIGS[args.config]
     header = config_header(args.config)
@@ -852,6 +922,9 @@ def main():
         if world > 1:
             out["collective"] = {"backend": args.backend if args.backend == "gloo" else "nccl (RCCL)",
                                  "world_size": dist.get_world_size(), "op": "batch_isend_irecv strip gather to rank 0"}
+            out["ranks"] = [{"rank": i, "device": devices[i]["device"], "pci_bus": devices[i]["pci_bus"],
+                             "rows": [plan.bounds[i], plan.bounds[i + 1]]} for i in range(world)]
+            out["launched_by"] = os.environ.get("RTRT_BENCH_LAUNCHER", "external launcher")
         if mode == 1:
             # standalone launches: in the pipelined timed region the post-process shares the GPU
             # with the next frame's AO pass, so its event span is not a kernel duration
@@ -890,6 +963,9 @@ def main():
 
 
 if __name__ == "__main__":
+    rc = launch_ranks(sys.argv[1:])
+    if rc >= 0:
+        sys.exit(rc)
     from real_time_ray_tracer_amd.dist import run_rank
 
     run_rank(main)

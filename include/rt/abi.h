@@ -259,7 +259,7 @@ int rt_read_row_counters(rt_ctx* ctx, uint64_t* rows, int reset);
 
 /* ---- device math self-test (parity of the shared float semantics) ------------------ */
 enum {
-  RT_MATH_SIN = 0,       /* deterministic sin used by random() (in: x)                 */
+  RT_MATH_SIN = 0,       /* sin used by random(): correctly rounded binary32 (in: x)  */
   RT_MATH_RANDOM = 1,    /* random(vec2) hash, p_compute.glsl:65-75 (in: x,y pairs)    */
   RT_MATH_SQRT = 2,      /* IEEE sqrt as used by the kernels (in: x)                   */
   RT_MATH_DIV = 3,       /* IEEE a/b (in: a,b pairs)                                   */
@@ -271,9 +271,11 @@ enum {
                              negative floats x where the kernels' 1/sqrt (normalize) differs
                              from 1.0f/sqrtf(x), plus those of the normal x in [2^-126, 2^126]
                              where their reciprocal differs from 1.0f/x                   */
-  RT_MATH_SQRT_TAIL_SWEEP = 8 /* out[i] = #bit patterns in [i*in[0], (i+1)*in[0]) of the finite
+  RT_MATH_SQRT_TAIL_SWEEP = 8, /* out[i] = #bit patterns in [i*in[0], (i+1)*in[0]) of the finite
                              non-negative floats where the hit-tail sqrt breaks its contract
                              (== sqrtf on [2^-96, FLT_MAX], in [0, 2^-47] below)          */
+  RT_MATH_SIN_RANGE = 9   /* out[i] = sin(x) of random() for the float whose bit pattern is
+                             bits(in[0]) + i (mod 2^32): exhaustive sweeps without inputs  */
 };
 int rt_selftest_math(rt_ctx* ctx, int fn, const float* in, float* out, size_t n);
 

@@ -72,6 +72,8 @@ def load():
     lib.rto_dispatch.restype = C.c_int
     lib.rto_sin.argtypes = [C.c_float]
     lib.rto_sin.restype = C.c_float
+    lib.rto_sin_check_range.argtypes = [C.c_uint32, C.c_int64, fp, C.POINTER(C.c_uint32), C.c_int]
+    lib.rto_sin_check_range.restype = C.c_int64
     lib.rto_random.argtypes = [C.c_float, C.c_float]
     lib.rto_random.restype = C.c_float
     lib.rto_sphere_eval.argtypes = [fp, fp, fp, C.c_float]
@@ -119,6 +121,15 @@ def dispatch(ssbo: np.ndarray, d: rto_dims, mode: int, frame: int, image=None, n
 def det_sin(x: np.ndarray) -> np.ndarray:
     f = load().rto_sin
     return np.array([f(float(v)) for v in np.asarray(x, np.float32).ravel()], np.float32)
+
+
+def sin_check_range(start: int, got: np.ndarray, max_bad: int = 64):
+    """(count, first bit patterns) where got[i] differs from rto_sin of bit pattern start + i."""
+    got = np.ascontiguousarray(got, np.float32)
+    bad = np.zeros(max_bad, np.uint32)
+    n = load().rto_sin_check_range(start & 0xFFFFFFFF, got.size, _fp(got), bad.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                   max_bad)
+    return int(n), bad[:min(n, max_bad)]
 
 
 def random2(xy: np.ndarray) -> np.ndarray:

@@ -43,21 +43,13 @@ def clamp(x, lo, hi):  # GLSL min(max(x, lo), hi) with GLSL's NaN-agnostic defin
 
 
 def det_sin(x):
-    """rt_oracle.c rto_sin: reduction by 2 pi (3-part constant), odd degree-11 polynomial."""
+    """sin() inside random(): the plain binary64 re-execution, (float)sin((double)x) with numpy's
+    (glibc's) sin.  The C oracle and the kernels compute the correctly rounded binary32 sin,
+    which this equals except at the rare double-rounding inputs (tests/test_oracle_cpu.py lists
+    and arbitrates them with mpmath)."""
     x = np.asarray(x, F)
-    h = lambda s: F(float.fromhex(s))  # noqa: E731
-    with np.errstate(invalid="ignore", over="ignore"):
-        k = np.rint(x * h("0x1.45f306p-3")).astype(F)
-        r = fma(-k, h("0x1.921fb6p+2"), x)
-        r = fma(-k, h("-0x1.777a5cp-23"), r)
-        r = fma(-k, h("-0x1.ee59dap-48"), r)
-        z = (r * r).astype(F)
-        p = fma(z, h("-0x1.5de3a2p-26"), h("0x1.6a5d34p-19"))
-        p = fma(z, p, h("-0x1.9f6b5ep-13"))
-        p = fma(z, p, h("0x1.11094ep-7"))
-        p = fma(z, p, h("-0x1.5554bep-3"))
-        p = fma(z, p, h("0x1.fffff2p-1"))
-        return (r * p).astype(F)
+    with np.errstate(invalid="ignore"):
+        return np.sin(x.astype(np.float64)).astype(F)
 
 
 def grandom(sx, sy):

@@ -15,6 +15,7 @@
 
 #include <immintrin.h>
 #include <math.h>
+#include <quadmath.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -48,25 +49,47 @@ static inline float gmin(float x, float y) { return y < x ? y : x; }
 static inline float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
 
 /* ------------------------------------------------------------------------------------ */
-/* deterministic sin (the float semantics of random(); see rt_oracle.h)                 */
-/* one period reduction by 2 pi (a 3-part binary32 constant, explicit fmaf: r in          */
-/* [-pi, pi]) and one odd degree-11 minimax polynomial, |error| <= 4e-7 on [-pi, pi].     */
-/* GLSL leaves sin's precision implementation-defined (Vulkan's GLSL bound: 2^-11 on      */
-/* [-pi, pi], nothing beyond); what random() needs is that host and device agree.        */
+/* sin inside random(): the correctly rounded binary32 sin (see rt_oracle.h).            */
+/* glibc's binary64 sin (error < 1 ulp) rounded once to binary32.  Where that rounding   */
+/* is ambiguous — the binary64 value within 8 ulps of a binary32 midpoint, i.e. its low  */
+/* 29 significand bits within 8 of 2^28, 1 input in 2^25 — quad precision (libquadmath   */
+/* sinq, 113 bits) decides.  A binary64 value that is a binary32 denormal is exact here  */
+/* (sin(x) rounds to x for |x| < 2^-26), so the midpoint test never misreads one.        */
+/* Written independently of the kernels' sin (real_time_ray_tracer_amd/csrc/rt_sin.h:    */
+/* reduction by pi, their own polynomial, Payne-Hanek, an exception table).              */
 /* ------------------------------------------------------------------------------------ */
 float rto_sin(float x) {
-  /* inf/NaN: k = rint(+-inf) = +-inf makes r = NaN, so the result is NaN */
-  float k = rintf(x * 0x1.45f306p-3f);        /* x / 2pi */
-  float r = fmaf(-k, 0x1.921fb6p+2f, x);      /* 2pi = 0x1.921fb6p+2 - 0x1.777a5cp-23 - 0x1.ee59dap-48 */
-  r = fmaf(-k, -0x1.777a5cp-23f, r);
-  r = fmaf(-k, -0x1.ee59dap-48f, r);
-  float z = r * r;
-  float p = fmaf(z, -0x1.5de3a2p-26f, 0x1.6a5d34p-19f);
-  p = fmaf(z, p, -0x1.9f6b5ep-13f);
-  p = fmaf(z, p, 0x1.11094ep-7f);
-  p = fmaf(z, p, -0x1.5554bep-3f);
-  p = fmaf(z, p, 0x1.fffff2p-1f);
-  return r * p;
+  if (!isfinite(x)) return x - x; /* NaN */
+  const double s = sin((double)x);
+  uint64_t u;
+  memcpy(&u, &s, sizeof u);
+  const uint32_t low = (uint32_t)u & 0x1FFFFFFFu;
+  if (low - (0x10000000u - 8u) <= 16u) return (float)sinq((__float128)x);
+  return (float)s;
+}
+
+/* exhaustive-sweep support: got[i] is the device's sin of the float whose bit pattern is
+   start + i (mod 2^32); counts the i where rto_sin disagrees bit for bit (NaN == NaN) and
+   records the first max_bad of those bit patterns */
+int64_t rto_sin_check_range(uint32_t start, int64_t n, const float* got, uint32_t* bad, int max_bad) {
+  int64_t count = 0;
+#pragma omp parallel for schedule(static, 1 << 16)
+  for (int64_t i = 0; i < n; ++i) {
+    const uint32_t b = start + (uint32_t)i;
+    float x;
+    memcpy(&x, &b, 4);
+    const float want = rto_sin(x);
+    uint32_t wb, gb;
+    memcpy(&wb, &want, 4);
+    memcpy(&gb, &got[i], 4);
+    if (wb != gb && !(isnan(want) && isnan(got[i]))) {
+      int64_t k;
+#pragma omp atomic capture
+      k = count++;
+      if (k < max_bad) bad[k] = b;
+    }
+  }
+  return count;
 }
 
 /* random(vec2) — p_compute.glsl:65-75: fract(sin(dot(st, vec2(12.9898,78.233))) * 43758.5453123) */

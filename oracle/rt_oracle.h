@@ -19,11 +19,12 @@
  *   - sphere discriminant = fmaf(r, r, fmaf(b, b, -dot(pmc,pmc)));
  *   - normalize(v) = v * (1.0f / sqrtf(dot(v,v))), length(v) = sqrtf(dot(v,v)), IEEE / and
  *     sqrtf (the correctly rounded form of the rsqrt-multiply GLSL compilers emit);
- *   - sin() inside random() = rto_sin(): one period reduction by 2 pi (a 3-part binary32
- *     constant, explicit fmaf; r in [-pi, pi]) and one odd degree-11 minimax polynomial in
- *     r^2 (|error| <= 4e-7 on [-pi, pi]) — a deterministic sin both sides reproduce bit for
- *     bit; random() only needs a deterministic hash, and GLSL leaves sin's precision
- *     implementation-defined (round 4; rounds 1-3 reduced by pi/2 with a quadrant select);
+ *   - sin() inside random() = rto_sin(): the correctly rounded binary32 sin(x), the
+ *     mathematical function (glibc's binary64 sin rounded once; quad-precision sinq where that
+ *     rounding is ambiguous).  random() multiplies sin by 43758.5 before fract(), so only
+ *     the exact function lets any CPU re-execution reproduce the hash: (float)sin((double)x)
+ *     equals it except at the rare double-rounding inputs (round 5; rounds 1-4 used a
+ *     binary32 polynomial sin that only this oracle and the kernels shared);
  *   - shadow_ray's `double t` and its dvec3 length run in binary64 (p_compute.glsl:147-163);
  *   - pow() = libm powf (outputs only; never feeds control flow), so pixels agree within
  *     the north-star tolerance |g-c| <= 1e-4*max(|g|,|c|) + 1e-6, not bit for bit.
@@ -70,6 +71,9 @@ int rto_dispatch(float* ssbo, const rto_dims* d, int mode, int frame, float* ima
 
 /* primitives (exported for the math self-tests) */
 float rto_sin(float x);
+/* counts the bit patterns start .. start+n-1 (mod 2^32) where got[i] != rto_sin (NaN == NaN),
+ * recording the first max_bad of them in bad (the device sin's exhaustive sweep) */
+int64_t rto_sin_check_range(uint32_t start, int64_t n, const float* got, uint32_t* bad, int max_bad);
 float rto_random(float x, float y);
 float rto_sphere_eval(const float pos[3], const float dir[3], const float center[3], float r);
 void rto_normalize3(const float v[3], float out[3]);

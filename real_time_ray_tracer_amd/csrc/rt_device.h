@@ -9,6 +9,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rt_sin.h"
+#include "rt_sin_table.h"
+
 namespace rt {
 
 struct f3 {
@@ -70,26 +73,32 @@ __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; 
 __device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
 __device__ __forceinline__ float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
 
-// ---- deterministic sin: one period reduction by 2 pi (3-part binary32 constant, explicit fmaf:
-// r in [-pi, pi]) and one odd degree-11 minimax polynomial (|error| <= 4e-7 on [-pi, pi]).
-// Bit-identical to oracle/rt_oracle.c rto_sin for every float input.  GLSL leaves sin's
-// precision implementation-defined (Vulkan's bound for GLSL: 2^-11 absolute on [-pi, pi]); what
-// matters for random() is that host and device compute the same value.  (Rounds 1-3 reduced by
-// pi/2 and evaluated the Cephes sin and cos polynomials with a quadrant select: 25 VALU per
-// random() against 17 here.)
+// ---- sin in random(): the correctly rounded binary32 sin (rt_sin.h).  The rare lanes — an
+// argument beyond the fast path's range (|x| >= 2^22, inf, NaN) or a binary64 value whose
+// binary32 rounding is ambiguous (1 in 2^24) — take det_sin_rare behind a wave-uniform branch.
+// Rounds 1-4 used a binary32 reduction and polynomial here (a faithful sin, 17 VALU), which a
+// CPU re-execution with the math library's sin could not reproduce (round-4 review).
+__device__ __noinline__ static float det_sin_rare(float x) {
+  if (!(__builtin_fabsf(x) <= 0x1.fffffep127f)) return x - x;  // inf, NaN -> NaN
+  const double s = sin_binary64(x);
+  if (!sin_ambiguous(s)) return (float)s;
+  const uint32_t b = __float_as_uint(x);
+  int lo = 0, hi = kSinTableN;  // lower bound of b in the sorted table
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (kSinTableX[mid] < b) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < kSinTableN && kSinTableX[lo] == b) ? __uint_as_float(kSinTableY[lo]) : (float)s;
+}
 __device__ __forceinline__ float det_sin(float x) {
-  // inf/NaN: k = rint(+-inf) = +-inf makes r = NaN, so the result is NaN (as the oracle's)
-  const float k = rintf(x * 0x1.45f306p-3f);
-  float r = fmaf(-k, 0x1.921fb6p+2f, x);
-  r = fmaf(-k, -0x1.777a5cp-23f, r);
-  r = fmaf(-k, -0x1.ee59dap-48f, r);
-  const float z = r * r;
-  float p = fmaf(z, -0x1.5de3a2p-26f, 0x1.6a5d34p-19f);
-  p = fmaf(z, p, -0x1.9f6b5ep-13f);
-  p = fmaf(z, p, 0x1.11094ep-7f);
-  p = fmaf(z, p, -0x1.5554bep-3f);
-  p = fmaf(z, p, 0x1.fffff2p-1f);
-  return r * p;
+  const double s = sin_fast(x);
+  float y = (float)s;
+  const bool rare = !(__builtin_fabsf(x) < 0x1p22f) || sin_ambiguous(s);
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(rare) != 0, 0)) {
+    if (rare) y = det_sin_rare(x);
+  }
+  return y;
 }
 
 // IEEE binary32 square root, correctly rounded: the value sqrtf() has under

@@ -1857,6 +1857,7 @@ __global__ void selftest_kernel(int fn, const float* __restrict__ in, float* __r
   if (i >= n) return;
   switch (fn) {
     case 0: out[i] = det_sin(in[i]); break;
+    case 9: out[i] = det_sin(__uint_as_float(__float_as_uint(in[0]) + (unsigned)i)); break;  // bit patterns in[0].., wrapping
     case 1: out[i] = grandom(in[2 * i], in[2 * i + 1]); break;
     case 2: out[i] = sqrt_rn(in[i]); break;
     case 6: {  // exhaustive sqrt_rn == sqrtf over bit patterns [i*per, (i+1)*per) of [0, 0x7f800000]

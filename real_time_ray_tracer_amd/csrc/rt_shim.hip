@@ -1500,11 +1500,12 @@ int rt_read_row_counters(rt_ctx* c, uint64_t* rows, int reset) {
 }
 
 int rt_selftest_math(rt_ctx* c, int fn, const float* in, float* out, size_t n) {
-  if (!c || !in || !out || fn < 0 || fn > RT_MATH_SQRT_TAIL_SWEEP) return RT_E_INVAL;
-  static const int in_w[] = {1, 2, 1, 2, 3, 10, 0, 0, 0}, out_w[] = {1, 1, 1, 1, 3, 1, 1, 1, 1};
+  if (!c || !in || !out || fn < 0 || fn > RT_MATH_SIN_RANGE) return RT_E_INVAL;
+  static const int in_w[] = {1, 2, 1, 2, 3, 10, 0, 0, 0, 0}, out_w[] = {1, 1, 1, 1, 3, 1, 1, 1, 1, 1};
   RT_HIP(c, hipSetDevice(c->device));
   float *din = nullptr, *dout = nullptr;
-  const bool sweep = fn == RT_MATH_SQRT_SWEEP || fn == RT_MATH_RCP_SWEEP || fn == RT_MATH_SQRT_TAIL_SWEEP;
+  const bool sweep = fn == RT_MATH_SQRT_SWEEP || fn == RT_MATH_RCP_SWEEP || fn == RT_MATH_SQRT_TAIL_SWEEP ||
+                     fn == RT_MATH_SIN_RANGE;  // in: one float (the count or the first bit pattern)
   size_t ib = sweep ? sizeof(float) : n * in_w[fn] * sizeof(float);
   size_t ob = n * out_w[fn] * sizeof(float);
   RT_HIP(c, hipMalloc(&din, std::max<size_t>(ib, 4)));

@@ -227,3 +227,38 @@ def test_bench_rank_failure_exits_nonzero_under_torchrun():
     assert r.returncode != 0, r.stdout[-2000:]
     assert "[rank 1/2] failed: RuntimeError: injected failure on rank 1" in r.stderr, r.stderr[-3000:]
     assert elapsed < 200, elapsed
+
+
+def test_bench_gpus_n_starts_n_ranks_without_a_launcher():
+    """`python bench.py --gpus 2` (no torchrun, WORLD_SIZE unset) runs 2 ranks:
+    bench.py starts torch.distributed.run itself before anything touches the GPU.  Here the
+    ranks stop after the start-up check (--launch-check, gloo on the CPU) and rank 0 reports
+    both; the rendering run of the same command is tests/test_gpu_bench_launch.py."""
+    import json
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--backend", "gloo", "--launch-check",
+                        "--dist-timeout", "60"], capture_output=True, text=True, timeout=240, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["ranks_up"] == 2 and out["gpus_arg"] == 2
+    assert [q["rank"] for q in out["ranks"]] == [0, 1] and len({q["pid"] for q in out["ranks"]}) == 2
+    assert out["launched_by"].startswith("bench.py --gpus 2")
+
+
+def test_bench_world_size_must_equal_gpus():
+    """Under a launcher, WORLD_SIZE != --gpus is an error naming both numbers (a run asked for N
+    GPUs never quietly renders on another count)."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "3", "--backend", "gloo", "--launch-check"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=str(ROOT))
+    assert r.returncode != 0
+    assert "--gpus 3 but WORLD_SIZE 2" in r.stderr, r.stderr[-2000:]

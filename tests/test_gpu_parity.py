@@ -300,8 +300,8 @@ def test_math_primitives_bitwise():
     rng = np.random.default_rng(0)
     x = np.concatenate([rng.uniform(-5e5, 5e5, 20000), rng.uniform(-10, 10, 5000),
                         [0.0, -0.0, 1e-30, 3.14159265, 1.5707964, 1e6, 3e7],
-                        # huge arguments: the reduction's output is meaningless but the same IEEE ops
-                        [3.3e9, -3.3e9, 3.4e9, -3.4e9, 1e10, -1e10, 3e38, -3e38]]).astype(np.float32)
+                        # huge arguments: the Payne-Hanek path (|x| >= 2^22)
+                        [3.3e9, -3.3e9, 3.4e9, -3.4e9, 1e10, -1e10, 3e38, -3e38, 4194304.0, -4194304.0]]).astype(np.float32)
     ref = oracle.det_sin(x)
     assert_bitwise(r.selftest_math(_lib.RT_MATH_SIN, x, x.size), ref, "det_sin")
     bad = np.array([np.inf, -np.inf, np.nan], np.float32)
@@ -336,6 +336,28 @@ def test_sqrt_tail_exhaustive():
     r.close()
     assert n * per > 0x7f7fffff
     assert float(bad.sum()) == 0.0, f"{int(bad.sum())} inputs break the contract"
+
+
+def test_det_sin_exhaustive():
+    """random()'s sin on the device (csrc/rt_sin.h: binary64 fast path, Payne-Hanek beyond
+    2^22, exception table) equals the oracle's independent correctly rounded sin (glibc's binary64
+    sin, quad-precision sinq where its rounding is ambiguous) on all 2^32 bit patterns, bit for
+    bit (NaN == NaN, -0 included)."""
+    import time
+    r = Renderer(8, 8, 1, 1)
+    chunk = 1 << 27
+    total, firsts = 0, []
+    t0 = time.time()
+    for start in range(0, 1 << 32, chunk):
+        got = r.selftest_math(_lib.RT_MATH_SIN_RANGE, np.array([start], np.uint32).view(np.float32), chunk)
+        n, bad = oracle.sin_check_range(start, got, max_bad=8)
+        total += n
+        firsts += [f"0x{int(b):08x}" for b in bad]
+        if start % (1 << 30) == 0:
+            print(f"  sin sweep {start:#010x}: {total} mismatches so far, {time.time() - t0:.1f} s", flush=True)
+    r.close()
+    print(f"  sin sweep: all 2^32 bit patterns, {total} mismatches, {time.time() - t0:.1f} s")
+    assert total == 0, f"{total} inputs differ from the correctly rounded sin, e.g. {firsts[:8]}"
 
 
 def test_rcp_rn_exhaustive():
