@@ -144,6 +144,9 @@ int rt_set_tile_schedule(rt_ctx* ctx, int on);
 /* 0 = off, 1 = on with row order still in use (no costs read back yet), 2 = a longest-first
  * order is in use. */
 int rt_tile_schedule_state(rt_ctx* ctx);
+/* how many longest-first orders have been taken up since the schedule was (re)enabled: each new
+ * order replaces a table that launches still in flight may read, so tests count the swaps */
+int rt_tile_schedule_orders(rt_ctx* ctx);
 /* Copy device state to the host in the REFERENCE layout.  Any pointer may be NULL.
  * pixels/normals/depth: [F][W][R] vec4 (x-major, y fastest; R = rows of this context),
  * image: [R][W] rgba32f (row 0 = row_begin, bottom-left origin like the GL texture). */

@@ -59,6 +59,7 @@ SIGNATURES = {
     "rt_set_frame_batch": (C.c_int, [_ctx, C.c_int]),
     "rt_set_tile_schedule": (C.c_int, [_ctx, C.c_int]),
     "rt_tile_schedule_state": (C.c_int, [_ctx]),
+    "rt_tile_schedule_orders": (C.c_int, [_ctx]),
     "rt_download": (C.c_int, [_ctx, _fp, _fp, _fp, _fp]),
     "rt_download_rect": (C.c_int, [_ctx, C.c_int, C.c_int, C.c_int, C.c_int, _fp, _fp, _fp, _fp]),
     "rt_upload_gbuffer": (C.c_int, [_ctx, _fp, _fp, _fp]),

@@ -73,9 +73,13 @@ __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; 
 __device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
 __device__ __forceinline__ float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
 
-// ---- sin in random(): the correctly rounded binary32 sin (rt_sin.h).  The rare lanes — an
-// argument beyond the fast path's range (|x| >= 2^22, inf, NaN) or a binary64 value whose
-// binary32 rounding is ambiguous (1 in 2^24) — take det_sin_rare behind a wave-uniform branch.
+// ---- sin in random(): the correctly rounded binary32 sin (rt_sin.h), in two tiers.  Tier 1
+// (det_sin_n): the binary64 reduction by pi and a degree-5 polynomial (relative error 2^-43.7),
+// rounded to binary32 when that rounding is unambiguous within 2048 binary64 ulps.  The rare
+// lanes — 1 in 2^17 ambiguous at tier 1, or an argument beyond the reduction's range (|x| >=
+// 2^22, inf, NaN) — take det_sin_rare behind a wave-uniform branch: rt_sin.h's degree-6 /
+// Payne-Hanek binary64 value, its 16-ulp ambiguity test, and the exception table.  Checked on
+// all 2^32 inputs against the oracle (tests/test_gpu_parity.py::test_det_sin_exhaustive).
 // Rounds 1-4 used a binary32 reduction and polynomial here (a faithful sin, 17 VALU), which a
 // CPU re-execution with the math library's sin could not reproduce (round-4 review).
 __device__ __noinline__ static float det_sin_rare(float x) {
@@ -90,15 +94,6 @@ __device__ __noinline__ static float det_sin_rare(float x) {
     else hi = mid;
   }
   return (lo < kSinTableN && kSinTableX[lo] == b) ? __uint_as_float(kSinTableY[lo]) : (float)s;
-}
-__device__ __forceinline__ float det_sin(float x) {
-  const double s = sin_fast(x);
-  float y = (float)s;
-  const bool rare = !(__builtin_fabsf(x) < 0x1p22f) || sin_ambiguous(s);
-  if (__builtin_expect(__builtin_amdgcn_ballot_w64(rare) != 0, 0)) {
-    if (rare) y = det_sin_rare(x);
-  }
-  return y;
 }
 
 // IEEE binary32 square root, correctly rounded: the value sqrtf() has under
@@ -148,11 +143,87 @@ __device__ __forceinline__ float sqrt_rn_tail(float x) {
   return sqrt_rn_core(xc);
 }
 
+// sin of N arguments at once (tier 1 above), the same operations per argument: each binary64 constant is
+// materialised once for the N (two s_mov_b32, or one v_mov_b64 for the polynomial's first step,
+// whose two constants cannot both be SGPR operands) and the N independent chains interleave.
+template <int N>
+__device__ __forceinline__ void det_sin_n(const float (&x)[N], float (&y)[N]) {
+  using namespace sinrn;
+  double r[N], kd[N], z[N], p[N];
+  const double ci = sconst(kInvPi);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    r[i] = (double)x[i];
+    kd[i] = __builtin_rint(fma(r[i], ci, 0.0));
+  }
+  const double pa = sconst(kPiA);
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = fma(-kd[i], pa, r[i]);
+  const double pb = sconst(kPiB);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    r[i] = fma(-kd[i], pb, r[i]);
+    z[i] = r[i] * r[i];
+  }
+  const double c5 = sconst(kQ5);
+  double c4 = sconst(kQ4);  // into a VGPR pair here (one v_mov_b64), not hoisted out of the loop
+  asm volatile("" : "+v"(c4));
+#pragma unroll
+  for (int i = 0; i < N; ++i) p[i] = fma(c5, z[i], c4);
+#define RT_SIN_STEP(c)                                        \
+  {                                                           \
+    const double cc = sconst(c);                              \
+    _Pragma("unroll") for (int i = 0; i < N; ++i) p[i] = fma(p[i], z[i], cc); \
+  }
+  RT_SIN_STEP(kQ3) RT_SIN_STEP(kQ2) RT_SIN_STEP(kQ1) RT_SIN_STEP(kQ0)
+#undef RT_SIN_STEP
+  bool rare = false;
+  double sv[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const double si = r[i] * fma(z[i], p[i], 1.0);  // sin_poly
+    sv[i] = dfrom(dbits(si) ^ ((uint64_t)(uint32_t)(int32_t)kd[i] << 63));
+    y[i] = (float)sv[i];
+    rare = rare || !(__builtin_fabsf(x[i]) < 0x1p22f) || sin_ambiguous<kSinFastAmbUlps>(sv[i]);
+  }
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(rare) != 0, 0)) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (!(__builtin_fabsf(x[i]) < 0x1p22f) || sin_ambiguous<kSinFastAmbUlps>(sv[i])) y[i] = det_sin_rare(x[i]);
+  }
+}
+__device__ __forceinline__ float det_sin(float x) {
+  float y[1];
+  det_sin_n<1>({x}, y);
+  return y[0];
+}
+
 // random(vec2), p_compute.glsl:65-75
 __device__ __forceinline__ float grandom(float sx, float sy) {
   float d = fmaf(sy, 78.233f, sx * 12.9898f);
   float m = det_sin(d) * 43758.5453123f;
   return m - floorf(m);
+}
+// N random() calls at once (det_sin_n); the same float operations per call as grandom
+#ifndef RT_SIN_WIDE
+#define RT_SIN_WIDE 1
+#endif
+template <int N>
+__device__ __forceinline__ void grandom_n(const float (&sx)[N], const float (&sy)[N], float (&out)[N]) {
+  float d[N], s[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) d[i] = fmaf(sy[i], 78.233f, sx[i] * 12.9898f);
+  if (RT_SIN_WIDE) {
+    det_sin_n<N>(d, s);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) s[i] = det_sin(d[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float m = s[i] * 43758.5453123f;
+    out[i] = m - floorf(m);
+  }
 }
 
 // ---- scene tables ---------------------------------------------------------------------

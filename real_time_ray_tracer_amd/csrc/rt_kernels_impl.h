@@ -1214,8 +1214,10 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       {  // ao_compute.glsl:310-323; sample 0 is unjittered: px + 0 == px, so one path for
         // every lane (no divergent branch in the batch)
         float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
-        float u = grandom(((s.x + px * f.z) - px) + f.x, ((f.y + py * s.w) - py) + s.y);
-        float w = grandom(s.z * px - (f.x * px) * f.z, f.w * py - (s.y * py) * s.w);
+        float uw[2];
+        grandom_n<2>({((s.x + px * f.z) - px) + f.x, s.z * px - (f.x * px) * f.z},
+                     {((f.y + py * s.w) - py) + s.y, f.w * py - (s.y * py) * s.w}, uw);
+        float u = uw[0], w = uw[1];
         normalize2(u, w);
         const float jx = aa == 0 ? 0.0f : div_rn_by(u, 6.0f, kInv6) - 0.08333f;
         const float jy = aa == 0 ? 0.0f : div_rn_by(w, 6.0f, kInv6) - 0.08333f;
@@ -1228,10 +1230,10 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       // hit uses it)
       auto hemisphere = [&]() {
         float4 f = rbuf[2 * aa], s = rbuf[2 * aa + 1];
-        float a = grandom(f.x + px * s.z, f.y + py * s.w);
-        float b = grandom(f.z - px * s.z, f.w - py * s.w);
-        float e = grandom(s.x * px + s.z, s.y * py + s.w);
-        return normalize(mk(a * 2.0f - 1.0f, b * 2.0f - 1.0f, e * 2.0f - 1.0f));
+        float abe[3];
+        grandom_n<3>({f.x + px * s.z, f.z - px * s.z, s.x * px + s.z}, {f.y + py * s.w, f.w - py * s.w, s.y * py + s.w},
+                     abe);
+        return normalize(mk(abe[0] * 2.0f - 1.0f, abe[1] * 2.0f - 1.0f, abe[2] * 2.0f - 1.0f));
       };
       if (!LAZY) bhemi = hemisphere();
       // the camera in VGPRs for the primary tests: with the uniform camera and the sphere both in

@@ -77,6 +77,7 @@ struct TileSched {
   int pending = -1;                    // the table being uploaded
   bool cost_inflight = false;
   long long launches = 0;
+  int orders_taken = 0;                // orders that became active (rt_tile_schedule_orders)
   std::vector<unsigned> cur, next;     // the active / pending order
 };
 constexpr int kSchedPeriod = 16;
@@ -396,22 +397,32 @@ int sched_before(rt_ctx* c, int kind, int gx, int gy, int per_unit, rt::FramePar
     RT_HIP(c, hipEventCreateWithFlags(&h.ev_cost, hipEventDisableTiming));
     RT_HIP(c, hipEventCreateWithFlags(&h.ev_order, hipEventDisableTiming));
   }
-  auto landed = [&](hipEvent_t e) {
+  // has the work before event e finished?  hipErrorNotReady is "not yet" (its per-thread error
+  // is cleared); any other failure is a fault of the side stream's copies or of the launches they
+  // wait on, reported to the caller (rt_last_hip_error), never taken as "not yet"
+  bool order_landed = false, cost_landed = false;
+  auto query = [&](hipEvent_t e, bool& done) -> hipError_t {
     const hipError_t q = hipEventQuery(e);
-    if (q == hipErrorNotReady) return false;
-    (void)hipGetLastError();
-    return q == hipSuccess;
+    done = q == hipSuccess;
+    if (q == hipErrorNotReady) {
+      (void)hipGetLastError();
+      return hipSuccess;
+    }
+    return q;
   };
-  if (h.pending >= 0 && landed(h.ev_order)) {
+  if (h.pending >= 0) RT_HIP(c, query(h.ev_order, order_landed));
+  if (h.cost_inflight) RT_HIP(c, query(h.ev_cost, cost_landed));
+  if (order_landed) {
     if (h.active >= 0)  // the launches enqueued so far are the old table's last readers
       for (int s = 0; s < 3; ++s)
         if (h.used_on[h.active][s]) RT_HIP(c, hipEventRecord(h.ev_use[h.active][s], h.used_on[h.active][s]));
     h.active = h.pending;
     h.pending = -1;
+    ++h.orders_taken;
     h.cur.swap(h.next);
     for (auto& st : h.used_on[h.active]) st = nullptr;
   }
-  if (h.cost_inflight && landed(h.ev_cost)) {
+  if (cost_landed) {
     h.cost_inflight = false;
     if (h.pending < 0) {
       // longest first: a unit's cost is its slowest slot's; ties keep the plain order
@@ -1251,6 +1262,13 @@ int rt_tile_schedule_state(rt_ctx* c) {
   for (auto& h : c->sched)
     if (h.active >= 0) return 2;
   return 1;
+}
+
+int rt_tile_schedule_orders(rt_ctx* c) {
+  if (!c) return RT_E_INVAL;
+  int n = 0;
+  for (auto& h : c->sched) n += h.orders_taken;
+  return n;
 }
 
 int rt_set_frame_batch(rt_ctx* c, int max_frames) {

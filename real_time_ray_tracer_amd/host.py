@@ -261,6 +261,10 @@ class Renderer:
         """0 off, 1 on (row order so far), 2 a longest-first order in use (rt_tile_schedule_state)."""
         return self._c(self._lib.rt_tile_schedule_state(self.ctx), "rt_tile_schedule_state")
 
+    def tile_schedule_orders(self) -> int:
+        """Orders taken up so far (rt_tile_schedule_orders)."""
+        return self._c(self._lib.rt_tile_schedule_orders(self.ctx), "rt_tile_schedule_orders")
+
     def download(self, pixels=True, normals=True, depth=True, image=True) -> GBuffer:
         shp = (self.F, self.W, self.R, 4)
         p = np.empty(shp, np.float32) if pixels else None

@@ -108,3 +108,75 @@ def test_tile_schedule_survives_a_stream_change():
     img2, state2 = run(False)
     assert state == 2 and state2 == 0
     assert np.array_equal(img.view(np.uint32), img2.view(np.uint32))
+
+
+def _two_poses():
+    """config (b) from its own camera and from a camera moved 6 units left and turned: the
+    mirror-bouncing tiles move, so the longest-first order changes with the pose"""
+    W, H, S, spp, mode, _ = CONFIGS["b"]
+    a = config_header("b")
+    b = a.copy()
+    b.camera_basis((-6.0, 1.0, 14.0), (0.0, 1.0, 0.0), (0.3, 0.0, 1.0), W / H)
+    return a, b
+
+
+def test_tile_schedule_order_swaps_keep_every_pixel():
+    """several order swaps in one run (the pose alternates every 32 frames), each
+    replacing the table that launches in flight may still read (ev_use / used_on): every 8th
+    frame's image and the final ring equal row order's bit for bit."""
+    W, H, S, spp, mode, _ = CONFIGS["b"]
+
+    def run(schedule):
+        a, b = _two_poses()
+        r = Renderer(W, H, S, spp)
+        r.set_tile_schedule(schedule)
+        f, imgs = 0, []
+        for k in range(224):
+            h = a if (k // 32) % 2 == 0 else b
+            h.moving_light(True)
+            h.set_mode(f, h.num_objects)
+            r.upload_header(h)
+            f = r.dispatch(mode, f)
+            if k % 8 == 7:
+                imgs.append(r.image())
+        pix = r.download(normals=False, depth=False, image=False).pixels
+        orders, state = r.tile_schedule_orders(), r.tile_schedule_state()
+        r.close()
+        return imgs, pix, orders, state
+
+    imgs, pix, orders, state = run(True)
+    imgs2, pix2, orders2, state2 = run(False)
+    print(f"orders taken up: {orders}")
+    assert state == 2 and orders >= 3, (state, orders)
+    assert state2 == 0 and orders2 == 0
+    for i, (x, y) in enumerate(zip(imgs, imgs2)):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), f"image after frame {8 * i + 7}"
+    assert np.array_equal(pix.view(np.uint32), pix2.view(np.uint32))
+
+
+def test_tile_schedule_with_multi_frame_launches():
+    """mode-4 launches of up to 32 frames (rt_set_frame_batch, rt_compute_frames) with
+    the schedule on, where every z-block of a launch writes the same cost slots: the ring and the
+    image equal row order's bit for bit."""
+    W, H, S, spp, mode, _ = CONFIGS["b"]
+
+    def run(schedule):
+        a, b = _two_poses()
+        r = Renderer(W, H, S, spp)
+        r.set_tile_schedule(schedule)
+        r.set_frame_batch(32)
+        f = 0
+        for k in range(12):
+            f = r.compute_frames(a if k % 4 < 2 else b, mode, f, 24, 7000, True)
+        r.synchronize()
+        g = r.download(normals=False, depth=False)
+        orders = r.tile_schedule_orders()
+        r.close()
+        return g, f, orders
+
+    g, f, orders = run(True)
+    g2, f2, _ = run(False)
+    print(f"orders taken up: {orders}")
+    assert f == f2
+    assert np.array_equal(g.image.view(np.uint32), g2.image.view(np.uint32))
+    assert np.array_equal(g.pixels.view(np.uint32), g2.pixels.view(np.uint32))

@@ -244,6 +244,12 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
   if (const char* eb = getenv("RTRT_HY_BLK"); eb && program == K_HYBRID && !pl) {  // block shape A/B
     const int k = atoi(eb);
     auto gr = [&](int bwx, int bwy) { return dim3((p.W + 8 * bwx - 1) / (8 * bwx), (p.trace_rows + 8 * bwy - 1) / (8 * bwy)); };
+    // the shim sizes the tile schedule's tables for the production 16x16 blocks of 4 waves
+    // (rt_shim.hip launch_sched): other shapes run in plain row order and record no costs
+    if (k == 11 || k == 21 || k == 41 || k == 42 || k == 44) {
+      q.tile_order = nullptr;
+      q.tile_cost = nullptr;
+    }
     const size_t lt = tab_lds_bytes(p);
     if (k == 11) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 1, 1>), gr(1, 1), dim3(64), lt, stream, q);
     else if (k == 21) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 2, 1>), gr(2, 1), dim3(128), lt, stream, q);
