@@ -72,8 +72,9 @@ def load():
     lib.rto_dispatch.restype = C.c_int
     lib.rto_sin.argtypes = [C.c_float]
     lib.rto_sin.restype = C.c_float
-    lib.rto_sin_check_range.argtypes = [C.c_uint32, C.c_int64, fp, C.POINTER(C.c_uint32), C.c_int]
-    lib.rto_sin_check_range.restype = C.c_int64
+    if hasattr(lib, "rto_sin_check_range"):  # (absent from older builds, tools/sin_change_effect.py)
+        lib.rto_sin_check_range.argtypes = [C.c_uint32, C.c_int64, fp, C.POINTER(C.c_uint32), C.c_int]
+        lib.rto_sin_check_range.restype = C.c_int64
     lib.rto_random.argtypes = [C.c_float, C.c_float]
     lib.rto_random.restype = C.c_float
     lib.rto_sphere_eval.argtypes = [fp, fp, fp, C.c_float]
