@@ -942,6 +942,11 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
 // and slot buffers, the image by the launch's last frame only.
 // CL: the bounce-ray cluster cull of the later bounce rounds (P.ncl > 0); without it the rounds
 // test every sphere.
+// waves per SIMD the production AO kernel is compiled for (its register budget: 7 -> 72 VGPRs)
+#ifndef RT_AO_MINW
+#define RT_AO_MINW 7
+#endif
+constexpr int kAoMinWaves = RT_AO_MINW;
 template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
           int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false, bool CL = true, int DC = 0,
           bool CLON = false>
@@ -1933,19 +1938,19 @@ inline void launch_batch(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStrea
   if (q.mf_n > 0) {  // multi-frame mode-2 launch (never with counters: rt_compute_frames checks)
     g.y = (unsigned)q.mf_n;
     if (tl)
-      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL, true, TLC, DC, CLON>), g, b, lds, stream, q, q.sph);
+      hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, true, true, SPPC, true, false, PL, true, TLC, DC, CLON>), g, b, lds, stream, q, q.sph);
     else
-      hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, false, PL, true, true, DC, CLON>), g, b, lds, stream, q, q.sph);
+      hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, GT, true, SPPC, false, false, PL, true, true, DC, CLON>), g, b, lds, stream, q, q.sph);
     return;
   }
   if (tl && cnt)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, true, PL, false, TLC, DC, CLON>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, true, true, SPPC, true, true, PL, false, TLC, DC, CLON>), g, b, lds, stream, q, q.sph);
   else if (tl)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, SPPC, true, false, PL, false, TLC, DC, CLON>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, true, true, SPPC, true, false, PL, false, TLC, DC, CLON>), g, b, lds, stream, q, q.sph);
   else if (cnt)
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, true, PL, false, true, DC, CLON>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, GT, true, SPPC, false, true, PL, false, true, DC, CLON>), g, b, lds, stream, q, q.sph);
   else
-    hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, GT, true, SPPC, false, false, PL, false, true, DC, CLON>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, GT, true, SPPC, false, false, PL, false, true, DC, CLON>), g, b, lds, stream, q, q.sph);
 }
 
 // g-buffer layout conversion (rt_download / rt_upload_gbuffer, the host-buffer path of
