@@ -151,11 +151,29 @@ __device__ __forceinline__ void det_sin_n(const float (&x)[N], float (&y)[N]) {
   using namespace sinrn;
   double r[N], kd[N], z[N], p[N];
   const double ci = sconst(kInvPi);
+#ifndef RT_SIN_MAGIC
+#define RT_SIN_MAGIC 1
+#endif
+#if RT_SIN_MAGIC
+  // k = x/pi rounded to an integer by adding 1.5*2^52 (one VGPR pair per group: a v_fma_f64 cannot
+  // take two SGPR constants): k's parity is bit 0 of the sum's low word, so no v_cvt_i32_f64
+  double rnd = sconst(0x1.8p52);
+  asm volatile("" : "+v"(rnd));
+  uint32_t par[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    r[i] = (double)x[i];
+    const double t = fma(r[i], ci, rnd);
+    par[i] = (uint32_t)dbits(t);
+    kd[i] = t - sconst(0x1.8p52);
+  }
+#else
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     r[i] = (double)x[i];
     kd[i] = __builtin_rint(fma(r[i], ci, 0.0));
   }
+#endif
   const double pa = sconst(kPiA);
 #pragma unroll
   for (int i = 0; i < N; ++i) r[i] = fma(-kd[i], pa, r[i]);
@@ -177,19 +195,22 @@ __device__ __forceinline__ void det_sin_n(const float (&x)[N], float (&y)[N]) {
   }
   RT_SIN_STEP(kQ3) RT_SIN_STEP(kQ2) RT_SIN_STEP(kQ1) RT_SIN_STEP(kQ0)
 #undef RT_SIN_STEP
-  bool rare = false;
-  double sv[N];
+  unsigned rare = 0;  // bit i: argument i goes to tier 2 (the binary64 values die here)
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const double si = r[i] * fma(z[i], p[i], 1.0);  // sin_poly
-    sv[i] = dfrom(dbits(si) ^ ((uint64_t)(uint32_t)(int32_t)kd[i] << 63));
-    y[i] = (float)sv[i];
-    rare = rare || !(__builtin_fabsf(x[i]) < 0x1p22f) || sin_ambiguous<kSinFastAmbUlps>(sv[i]);
+#if RT_SIN_MAGIC
+    const double sv = dfrom(dbits(si) ^ ((uint64_t)par[i] << 63));
+#else
+    const double sv = dfrom(dbits(si) ^ ((uint64_t)(uint32_t)(int32_t)kd[i] << 63));
+#endif
+    y[i] = (float)sv;
+    rare |= (unsigned)(!(__builtin_fabsf(x[i]) < 0x1p22f) || sin_ambiguous<kSinFastAmbUlps>(sv)) << i;
   }
-  if (__builtin_expect(__builtin_amdgcn_ballot_w64(rare) != 0, 0)) {
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(rare != 0) != 0, 0)) {
 #pragma unroll
     for (int i = 0; i < N; ++i)
-      if (!(__builtin_fabsf(x[i]) < 0x1p22f) || sin_ambiguous<kSinFastAmbUlps>(sv[i])) y[i] = det_sin_rare(x[i]);
+      if ((rare >> i) & 1u) y[i] = det_sin_rare(x[i]);
   }
 }
 __device__ __forceinline__ float det_sin(float x) {

@@ -873,7 +873,25 @@ __global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(FrameParams P) {
     else stage_shapes(P, lds);
     __syncthreads();
   }
-  if constexpr (kHybridTilesPerBlock > 1) {  // A/B builds: TPB vertically adjacent tiles per block
+  if constexpr (kHybridTilesPerBlock == 2) {
+    // A/B builds: two tiles per block, half the waves.  Block b takes the tiles at positions b and
+    // n - 1 - b of the schedule's order (row order without one): one of the longest with one of
+    // the shortest, so block durations stay even.  The grid is gx x ceil(gy / 2).
+    const unsigned gx = gridDim.x, gy = (unsigned)(P.trace_rows + 8 * BWY - 1) / (8 * BWY), n = gx * gy;
+    const unsigned b = blockIdx.x + blockIdx.y * gx;
+#pragma unroll 1
+    for (int t = 0; t < 2; ++t) {
+      const unsigned u = t == 0 ? b : n - 1 - b;
+      if (b > n - 1 - b || (t == 1 && u == b)) break;  // (block-uniform; blocks past n / 2 have no tiles)
+      unsigned bx = u % gx, by = u / gx;
+      if (P.tile_order) {
+        const unsigned v = P.tile_order[u];
+        bx = v & 0xffffu;
+        by = v >> 16;
+      }
+      hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), bx, by, frame_dst(P, blockIdx.z));
+    }
+  } else if constexpr (kHybridTilesPerBlock > 1) {  // A/B builds: TPB vertically adjacent tiles per block
 #pragma unroll 1
     for (int t = 0; t < kHybridTilesPerBlock; ++t)
       hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x,
