@@ -2072,7 +2072,19 @@ inline hipError_t launch_production(int program, const FrameParams& p, const Fra
   const int tpb = program == K_HYBRID ? kHybridTilesPerBlock : 1;
   dim3 grid((p.W + 15) / 16, ((p.trace_rows + 15) / 16 + tpb - 1) / tpb, p.mf_n > 0 ? (p.mf_n + fpb - 1) / fpb : 1);
   // scenes of at most kTabLdsMax objects: the tables staged in LDS per wave (LT)
-  const bool lt = p.nobj <= kTabLdsMax;
+// Modes 3/4 read the shape tables through the caches (scalar loads for the wave-uniform culls
+// and survivor tests, vector loads for the hit's material) instead of staging them in LDS per
+// block: no staging round trip and no block barrier before a wave's first test.  Round 5,
+// burst A/Bs: hybrid (b) 28.15 -> 26.78 us per launch (-4.9%), phong (a) 6.87 -> 6.75 us
+// (-1.7%), bit-identical (profiles/r05n_*).  Round 2 had measured the LDS tables faster
+// (40.4 -> 37.9 us) on the kernels of that time.  0 restores the LDS tables (A/B builds).
+#ifndef RT_HY_NOLT
+#define RT_HY_NOLT 1
+#endif
+#ifndef RT_PH_NOLT
+#define RT_PH_NOLT 1
+#endif
+  const bool lt = p.nobj <= kTabLdsMax && !(RT_HY_NOLT && program == K_HYBRID) && !(RT_PH_NOLT && program == K_PHONG);
   const size_t ltb = lt ? tab_lds_bytes(p) : 0;
   switch (program) {
     case K_PHONG:
