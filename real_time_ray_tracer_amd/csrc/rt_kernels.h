@@ -13,6 +13,15 @@ namespace rt {
 
 constexpr int kMaxFrames = 16;
 constexpr int kMaxBatch = 32;  // frames per multi-frame Phong/hybrid launch
+// Hybrid (mode 4) workgroups of kHyBW x kHyBW waves, each wave an 8x8 pixel tile; the tile
+// schedule's units are these workgroups (rt_shim launch_sched).  2x2 (16x16 pixels, 4 waves).
+// Round 5 A/Bs at (b), tables read through the caches: in row order 1x1 33.1, 2x1 33.6, 2x2 34.2,
+// 4x1 33.7, 4x2 35.0 us per launch (profiles/r05o_*), but with the longest-first schedule 1x1
+// (its order at 8x8 granularity) 28.3 vs 2x2 26.5 us (r05p_*).  Set for both translation units.
+#ifndef RT_HY_BW
+#define RT_HY_BW 2
+#endif
+constexpr int kHyBW = RT_HY_BW, kHyTile = 8 * RT_HY_BW;
 constexpr int kCounters = 8;
 constexpr int kCounterSlots = 256;  // per counter, summed by the host
 

@@ -209,7 +209,8 @@ constexpr int kPhongFramesPerBlock = 4, kHybridFramesPerBlock = 1;
 #ifndef RT_HY_TPB
 #define RT_HY_TPB 1
 #endif
-constexpr int kHybridTilesPerBlock = RT_HY_TPB;  // 16x16 tiles per hybrid block, one after another
+constexpr int kHybridTilesPerBlock = RT_HY_TPB;  // tiles per hybrid block, one after another (A/B)
+
 template <int FPB>
 __device__ __forceinline__ int block_frames(const FrameParams& P, int& j0) {
   if (P.mf_n <= 0) {
@@ -2070,7 +2071,10 @@ inline hipError_t launch_production(int program, const FrameParams& p, const Fra
   // modes 3/4 multi-frame launches: FPB frames per block (block_frames)
   const int fpb = program == K_PHONG ? kPhongFramesPerBlock : kHybridFramesPerBlock;
   const int tpb = program == K_HYBRID ? kHybridTilesPerBlock : 1;
-  dim3 grid((p.W + 15) / 16, ((p.trace_rows + 15) / 16 + tpb - 1) / tpb, p.mf_n > 0 ? (p.mf_n + fpb - 1) / fpb : 1);
+  // hybrid blocks: kHyBW x kHyBW waves of 8x8 pixels (kHyTile = 8 kHyBW px); phong: 2x2 waves
+  const int tw = program == K_HYBRID ? kHyTile : 16;
+  dim3 grid((p.W + tw - 1) / tw, ((p.trace_rows + tw - 1) / tw + tpb - 1) / tpb, p.mf_n > 0 ? (p.mf_n + fpb - 1) / fpb : 1);
+  const dim3 hyb(64 * kHyBW * kHyBW);
   // scenes of at most kTabLdsMax objects: the tables staged in LDS per wave (LT)
 // Modes 3/4 read the shape tables through the caches (scalar loads for the wave-uniform culls
 // and survivor tests, vector loads for the hit's material) instead of staging them in LDS per
@@ -2094,10 +2098,10 @@ inline hipError_t launch_production(int program, const FrameParams& p, const Fra
       else hipLaunchKernelGGL((phong_kernel<true, false, false>), grid, dim3(kBlock), 0, stream, q);
       break;
     case K_HYBRID:
-      if (pl && lt) hipLaunchKernelGGL((hybrid_kernel<true, true, true>), grid, dim3(kBlock), ltb, stream, q);
-      else if (pl) hipLaunchKernelGGL((hybrid_kernel<true, true, false>), grid, dim3(kBlock), 0, stream, q);
-      else if (lt) hipLaunchKernelGGL((hybrid_kernel<true, false, true>), grid, dim3(kBlock), ltb, stream, q);
-      else hipLaunchKernelGGL((hybrid_kernel<true, false, false>), grid, dim3(kBlock), 0, stream, q);
+      if (pl && lt) hipLaunchKernelGGL((hybrid_kernel<true, true, true, 0, kHyBW, kHyBW>), grid, hyb, ltb, stream, q);
+      else if (pl) hipLaunchKernelGGL((hybrid_kernel<true, true, false, 0, kHyBW, kHyBW>), grid, hyb, 0, stream, q);
+      else if (lt) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, kHyBW, kHyBW>), grid, hyb, ltb, stream, q);
+      else hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, kHyBW, kHyBW>), grid, hyb, 0, stream, q);
       break;
     case K_POST:
       hipLaunchKernelGGL(post_kernel,

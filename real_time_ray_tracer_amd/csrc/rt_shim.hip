@@ -485,11 +485,11 @@ int sched_after(rt_ctx* c, int kind, hipStream_t st) {
 // A launch of `program` with its schedule (hybrid tiles, AO pools), if it has one.
 int launch_sched(rt_ctx* c, int program, rt::FrameParams& p, hipStream_t st) {
   int kind = -1, gx = 0, gy = 1, per = 1;
-  if (program == RT_PROG_H_COMPUTE) {
+  if (program == RT_PROG_H_COMPUTE) {  // units: the hybrid workgroups (rt::kHyTile px square, kHyBW^2 waves)
     kind = kSchedHybrid;
-    gx = (p.W + 15) / 16;
-    gy = (p.trace_rows + 15) / 16;
-    per = 4;
+    gx = (p.W + rt::kHyTile - 1) / rt::kHyTile;
+    gy = (p.trace_rows + rt::kHyTile - 1) / rt::kHyTile;
+    per = rt::kHyBW * rt::kHyBW;
   }
   // (AO pools in the same longest-first order by wave time measured nothing at (c) and (d): those
   // launches are not tail-bound; the kernel's bookkeeping cost registers, profiles/r04h_*)

@@ -232,6 +232,10 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
   if (const char* ea = getenv("RTRT_HY_ABL"); ea && program == K_HYBRID && !pl && atoi(ea) > 0) {
     const int a = atoi(ea);
     const size_t lt = tab_lds_bytes(p);
+    if (kHyBW != 2) {  // 2x2 blocks here; the schedule's tables are sized for the production blocks
+      q.tile_order = nullptr;
+      q.tile_cost = nullptr;
+    }
     if (a == 1) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 1>), grid, dim3(kBlock), lt, stream, q);
     else if (a == 3) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 3>), grid, dim3(kBlock), lt, stream, q);
     else if (a == 5) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 5>), grid, dim3(kBlock), lt, stream, q);
@@ -244,19 +248,20 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
   if (const char* eb = getenv("RTRT_HY_BLK"); eb && program == K_HYBRID && !pl) {  // block shape A/B
     const int k = atoi(eb);
     auto gr = [&](int bwx, int bwy) { return dim3((p.W + 8 * bwx - 1) / (8 * bwx), (p.trace_rows + 8 * bwy - 1) / (8 * bwy)); };
-    // the shim sizes the tile schedule's tables for the production 16x16 blocks of 4 waves
-    // (rt_shim.hip launch_sched): other shapes run in plain row order and record no costs
-    if (k == 11 || k == 21 || k == 41 || k == 42 || k == 44) {
+    // the shim sizes the tile schedule's tables for the production blocks (kHyBW x kHyBW waves,
+    // rt_shim.hip launch_sched): other shapes run in plain row order and record no costs
+    const int bw = k / 10, bh = k % 10;
+    if (bw != kHyBW || bh != kHyBW) {
       q.tile_order = nullptr;
       q.tile_cost = nullptr;
     }
-    const size_t lt = tab_lds_bytes(p);
-    if (k == 11) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 1, 1>), gr(1, 1), dim3(64), lt, stream, q);
-    else if (k == 21) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 2, 1>), gr(2, 1), dim3(128), lt, stream, q);
-    else if (k == 41) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 4, 1>), gr(4, 1), dim3(256), lt, stream, q);
-    else if (k == 42) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 4, 2>), gr(4, 2), dim3(512), lt, stream, q);
-    else if (k == 44) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 4, 4>), gr(4, 4), dim3(1024), lt, stream, q);
-    else hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, 2, 2>), grid, dim3(kBlock), lt, stream, q);
+    // (tables through the caches, as production since round 5: RT_HY_NOLT)
+    if (k == 11) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 1, 1>), gr(1, 1), dim3(64), 0, stream, q);
+    else if (k == 21) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 2, 1>), gr(2, 1), dim3(128), 0, stream, q);
+    else if (k == 41) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 4, 1>), gr(4, 1), dim3(256), 0, stream, q);
+    else if (k == 42) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 4, 2>), gr(4, 2), dim3(512), 0, stream, q);
+    else if (k == 44) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 4, 4>), gr(4, 4), dim3(1024), 0, stream, q);
+    else hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 2, 2>), gr(2, 2), dim3(256), 0, stream, q);
     return hipGetLastError();
   }
   if (ab_general() && (program == K_PHONG || program == K_HYBRID)) {

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--libs", default="")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--no-schedule", action="store_true", help="tile schedule off (row order) for every variant")
     a = ap.parse_args()
     W, H, S, spp, mode, _ = CONFIGS[a.config]
     prog = {3: 4, 4: 5}[mode]
@@ -56,6 +57,8 @@ def main():
                 os.environ[a.env] = v
             h = config_header(a.config)
             r = Renderer(W, H, S, spp)
+            if a.no_schedule:
+                r.set_tile_schedule(False)
             f = 0
             for k in range(64):
                 h.moving_light(True)
