@@ -27,6 +27,13 @@ lib: $(LIB)
 oracle: $(ORACLE) $(ORACLE_NATIVE)
 headless: $(HEADLESS)
 
+# kernels whose leading arguments are scalars (hybrid_kernel's tables, selftest_kernel) get
+# them preloaded into SGPRs at wave launch (gfx950 kernarg preload; FrameParams is never preloaded)
+KARG_PRELOAD ?= -mllvm -amdgpu-kernarg-preload-count=7
+
+$(OBJDIR)/rt_kernels.o: $(CSRC)/rt_kernels.hip $(CSRC)/*.h include/rt/*.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(KARG_PRELOAD) -x hip -c $< -o $@
+
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(CSRC)/*.h include/rt/*.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
@@ -47,7 +54,7 @@ $(LIB): $(OBJDIR)/rt_kernels.o $(OBJDIR)/rt_shim.o $(OBJDIR)/rt_host.o $(OBJDIR)
 
 ABLIB := build/librtrt_ab.so
 $(OBJDIR)/rt_kernels_ab.o: tools/ab/rt_kernels_ab.hip $(CSRC)/*.h include/rt/*.h | $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -I$(CSRC) -x hip -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(KARG_PRELOAD) -I$(CSRC) -x hip -c $< -o $@
 
 $(ABLIB): $(OBJDIR)/rt_kernels_ab.o $(OBJDIR)/rt_shim.o $(OBJDIR)/rt_host.o $(OBJDIR)/rt_group.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread

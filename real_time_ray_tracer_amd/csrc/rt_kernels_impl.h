@@ -750,10 +750,11 @@ __device__ __forceinline__ void bounce_round(const FrameParams& P, const float4*
 // 3 = primary cull only, 5 = no bounce segments, 6 = bounces without the split rounds
 template <bool ALLSPH, bool PL, bool LT, int ABL = 0, int BWX = 2, int BWY = 2>
 __device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* lds, int* perm, int bx, int by,
-                                            const FrameDst& fd) {
+                                            const FrameDst& fd, const float4* __restrict__ gsph,
+                                            const float4* __restrict__ gshp) {
   const int n = P.nobj;  // !ALLSPH or LT: LDS tables (see phong_kernel)
-  const float4* tab = (ALLSPH && !LT) ? P.shapes : lds;
-  const float4* geo = (ALLSPH && !LT) ? P.sph : (ALLSPH ? lds + 4 * n : lds);
+  const float4* tab = (ALLSPH && !LT) ? gshp : lds;
+  const float4* geo = (ALLSPH && !LT) ? gsph : (ALLSPH ? lds + 4 * n : lds);
   const int stride = (ALLSPH && !LT) ? P.S : n;
   const float4 *geo2 = tab + stride, *col = tab + 2 * stride, *aux = tab + 3 * stride;
   int x, y;
@@ -865,8 +866,15 @@ __device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* 
   }
 }
 
+// The schedule's order table and the sphere / shape tables lead the argument list: the build
+// preloads the first kernel arguments into SGPRs (-mllvm -amdgpu-kernarg-preload-count, Makefile),
+// so a wave's first loads (its tile, then the culls' sphere rows) need not wait for a kernarg load.
+// (FrameParams, an aggregate, is never preloaded.)
 template <bool ALLSPH, bool PL = false, bool LT = false, int ABL = 0, int BWX = 2, int BWY = 2>
-__global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(FrameParams P) {
+__global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(const unsigned* __restrict__ tord,
+                                                                const float4* __restrict__ gsph,
+                                                                const float4* __restrict__ gshp, unsigned gx,
+                                                                FrameParams P) {
   extern __shared__ float4 lds[];
   __shared__ int hperm[64 * BWX * BWY];  // bounce_round's live-rank -> lane map, a slice per wave
   if (!ALLSPH || LT) {
@@ -885,38 +893,38 @@ __global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(FrameParams P) {
       const unsigned u = t == 0 ? b : n - 1 - b;
       if (b > n - 1 - b || (t == 1 && u == b)) break;  // (block-uniform; blocks past n / 2 have no tiles)
       unsigned bx = u % gx, by = u / gx;
-      if (P.tile_order) {
-        const unsigned v = P.tile_order[u];
+      if (tord) {
+        const unsigned v = tord[u];
         bx = v & 0xffffu;
         by = v >> 16;
       }
-      hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), bx, by, frame_dst(P, blockIdx.z));
+      hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), bx, by, frame_dst(P, blockIdx.z), gsph, gshp);
     }
   } else if constexpr (kHybridTilesPerBlock > 1) {  // A/B builds: TPB vertically adjacent tiles per block
 #pragma unroll 1
     for (int t = 0; t < kHybridTilesPerBlock; ++t)
       hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x,
-                                                 blockIdx.y * kHybridTilesPerBlock + t, frame_dst(P, blockIdx.z));
+                                                 blockIdx.y * kHybridTilesPerBlock + t, frame_dst(P, blockIdx.z), gsph, gshp);
   } else if constexpr (kHybridFramesPerBlock == 1) {  // no frame loop (the loop form costs 3-4% at (b))
     // the host's tile schedule (longest first, from the previous frames' bounce rounds): the
     // few tiles whose mirror paths bounce for many rounds start early instead of setting the
     // launch's tail (config (b): 32.0 -> 25.4 us per frame with the reverse of row order, which
     // happens to put that scene's bouncing tiles first)
     unsigned bx = blockIdx.x, by = blockIdx.y;
-    if (P.tile_order) {
-      const unsigned t = P.tile_order[blockIdx.x + blockIdx.y * gridDim.x];
+    if (tord) {
+      const unsigned t = tord[blockIdx.x + blockIdx.y * gx];  // (gx = gridDim.x, a preloaded argument)
       bx = t & 0xffffu;
       by = t >> 16;
     }
     hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), bx, by,
-                                               frame_dst(P, blockIdx.z));
+                                               frame_dst(P, blockIdx.z), gsph, gshp);
   } else {
     int j0;
     const int nj = block_frames<kHybridFramesPerBlock>(P, j0);
 #pragma unroll 1
     for (int j = 0; j < nj; ++j)
       hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), blockIdx.x, blockIdx.y,
-                                                 frame_dst(P, j0 + j));
+                                                 frame_dst(P, j0 + j), gsph, gshp);
   }
 }
 
@@ -2098,10 +2106,10 @@ inline hipError_t launch_production(int program, const FrameParams& p, const Fra
       else hipLaunchKernelGGL((phong_kernel<true, false, false>), grid, dim3(kBlock), 0, stream, q);
       break;
     case K_HYBRID:
-      if (pl && lt) hipLaunchKernelGGL((hybrid_kernel<true, true, true, 0, kHyBW, kHyBW>), grid, hyb, ltb, stream, q);
-      else if (pl) hipLaunchKernelGGL((hybrid_kernel<true, true, false, 0, kHyBW, kHyBW>), grid, hyb, 0, stream, q);
-      else if (lt) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, kHyBW, kHyBW>), grid, hyb, ltb, stream, q);
-      else hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, kHyBW, kHyBW>), grid, hyb, 0, stream, q);
+      if (pl && lt) hipLaunchKernelGGL((hybrid_kernel<true, true, true, 0, kHyBW, kHyBW>), grid, hyb, ltb, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+      else if (pl) hipLaunchKernelGGL((hybrid_kernel<true, true, false, 0, kHyBW, kHyBW>), grid, hyb, 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+      else if (lt) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, kHyBW, kHyBW>), grid, hyb, ltb, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+      else hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, kHyBW, kHyBW>), grid, hyb, 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
       break;
     case K_POST:
       hipLaunchKernelGGL(post_kernel,

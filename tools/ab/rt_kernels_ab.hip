@@ -236,13 +236,13 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
       q.tile_order = nullptr;
       q.tile_cost = nullptr;
     }
-    if (a == 1) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 1>), grid, dim3(kBlock), lt, stream, q);
-    else if (a == 3) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 3>), grid, dim3(kBlock), lt, stream, q);
-    else if (a == 5) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 5>), grid, dim3(kBlock), lt, stream, q);
-    else if (a == 6) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 6>), grid, dim3(kBlock), lt, stream, q);
-    else if (a == 7) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 7>), grid, dim3(kBlock), lt, stream, q);
-    else if (a == 8) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 7>), grid, dim3(kBlock), 0, stream, q);
-    else hipLaunchKernelGGL((hybrid_kernel<true, false, true, 2>), grid, dim3(kBlock), lt, stream, q);
+    if (a == 1) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 1>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+    else if (a == 3) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 3>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+    else if (a == 5) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 5>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+    else if (a == 6) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 6>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+    else if (a == 7) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 7>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+    else if (a == 8) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 7>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+    else hipLaunchKernelGGL((hybrid_kernel<true, false, true, 2>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
     return hipGetLastError();
   }
   if (const char* eb = getenv("RTRT_HY_BLK"); eb && program == K_HYBRID && !pl) {  // block shape A/B
@@ -256,18 +256,18 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
       q.tile_cost = nullptr;
     }
     // (tables through the caches, as production since round 5: RT_HY_NOLT)
-    if (k == 11) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 1, 1>), gr(1, 1), dim3(64), 0, stream, q);
-    else if (k == 21) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 2, 1>), gr(2, 1), dim3(128), 0, stream, q);
-    else if (k == 41) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 4, 1>), gr(4, 1), dim3(256), 0, stream, q);
-    else if (k == 42) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 4, 2>), gr(4, 2), dim3(512), 0, stream, q);
-    else if (k == 44) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 4, 4>), gr(4, 4), dim3(1024), 0, stream, q);
-    else hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 2, 2>), gr(2, 2), dim3(256), 0, stream, q);
+    if (k == 11) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 1, 1>), gr(1, 1), dim3(64), 0, stream, q.tile_order, q.sph, q.shapes, gr(1, 1).x, q);
+    else if (k == 21) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 2, 1>), gr(2, 1), dim3(128), 0, stream, q.tile_order, q.sph, q.shapes, gr(2, 1).x, q);
+    else if (k == 41) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 4, 1>), gr(4, 1), dim3(256), 0, stream, q.tile_order, q.sph, q.shapes, gr(4, 1).x, q);
+    else if (k == 42) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 4, 2>), gr(4, 2), dim3(512), 0, stream, q.tile_order, q.sph, q.shapes, gr(4, 2).x, q);
+    else if (k == 44) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 4, 4>), gr(4, 4), dim3(1024), 0, stream, q.tile_order, q.sph, q.shapes, gr(4, 4).x, q);
+    else hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, 2, 2>), gr(2, 2), dim3(256), 0, stream, q.tile_order, q.sph, q.shapes, gr(2, 2).x, q);
     return hipGetLastError();
   }
   if (ab_general() && (program == K_PHONG || program == K_HYBRID)) {
     const size_t lds = shapes_lds_bytes(p);
     if (program == K_PHONG) hipLaunchKernelGGL((phong_kernel<false>), grid, dim3(kBlock), lds, stream, q);
-    else hipLaunchKernelGGL((hybrid_kernel<false>), grid, dim3(kBlock), lds, stream, q);
+    else hipLaunchKernelGGL((hybrid_kernel<false>), grid, dim3(kBlock), lds, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
     return hipGetLastError();
   }
   return launch_production(program, p, q, stream);
