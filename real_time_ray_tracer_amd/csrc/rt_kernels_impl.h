@@ -594,10 +594,11 @@ __device__ __forceinline__ bool shadow_lit_sph(const FrameParams& P, const float
 // the spheres).  !ALLSPH (A/B builds only): the whole shape table staged in LDS, every shape
 // tested through eval_ray's id dispatch, no culling.
 template <bool ALLSPH, bool PL, bool LT, int BWX = 2, int BWY = 2>
-__device__ __forceinline__ void phong_tile(const FrameParams& P, const float4* lds, int bx, int by, const FrameDst& fd) {
+__device__ __forceinline__ void phong_tile(const FrameParams& P, const float4* lds, int bx, int by, const FrameDst& fd,
+                                           const float4* __restrict__ gsph, const float4* __restrict__ gshp) {
   const int n = P.nobj;
-  const float4* tab = (ALLSPH && !LT) ? P.shapes : lds;                       // geo | geo2 | col
-  const float4* geo = (ALLSPH && !LT) ? P.sph : (ALLSPH ? lds + 4 * n : lds);  // what the sphere tests read
+  const float4* tab = (ALLSPH && !LT) ? gshp : lds;                       // geo | geo2 | col
+  const float4* geo = (ALLSPH && !LT) ? gsph : (ALLSPH ? lds + 4 * n : lds);  // what the sphere tests read
   const int stride = (ALLSPH && !LT) ? P.S : n;
   const float4 *geo2 = tab + stride, *col = tab + 2 * stride;
   int x, y;
@@ -654,8 +655,10 @@ __device__ __forceinline__ void stage_tables(const FrameParams& P, float4* lds) 
   for (int k = threadIdx.x; k < n; k += blockDim.x) lds[4 * n + k] = P.sph[k];
 }
 
+// (the sphere and shape tables lead the arguments: preloaded into SGPRs, as for hybrid_kernel)
 template <bool ALLSPH, bool PL = false, bool LT = false>
-__global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
+__global__ __launch_bounds__(kBlock) void phong_kernel(const float4* __restrict__ gsph, const float4* __restrict__ gshp,
+                                                       FrameParams P) {
   extern __shared__ float4 lds[];
   if (!ALLSPH || LT) {
     if (LT) stage_tables(P, lds);
@@ -665,7 +668,8 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(FrameParams P) {
   int j0;
   const int nj = block_frames<kPhongFramesPerBlock>(P, j0);
 #pragma unroll 1
-  for (int j = 0; j < nj; ++j) phong_tile<ALLSPH, PL, LT>(P, lds, blockIdx.x, blockIdx.y, frame_dst(P, j0 + j));
+  for (int j = 0; j < nj; ++j)
+    phong_tile<ALLSPH, PL, LT>(P, lds, blockIdx.x, blockIdx.y, frame_dst(P, j0 + j), gsph, gshp);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2100,10 +2104,10 @@ inline hipError_t launch_production(int program, const FrameParams& p, const Fra
   const size_t ltb = lt ? tab_lds_bytes(p) : 0;
   switch (program) {
     case K_PHONG:
-      if (pl && lt) hipLaunchKernelGGL((phong_kernel<true, true, true>), grid, dim3(kBlock), ltb, stream, q);
-      else if (pl) hipLaunchKernelGGL((phong_kernel<true, true, false>), grid, dim3(kBlock), 0, stream, q);
-      else if (lt) hipLaunchKernelGGL((phong_kernel<true, false, true>), grid, dim3(kBlock), ltb, stream, q);
-      else hipLaunchKernelGGL((phong_kernel<true, false, false>), grid, dim3(kBlock), 0, stream, q);
+      if (pl && lt) hipLaunchKernelGGL((phong_kernel<true, true, true>), grid, dim3(kBlock), ltb, stream, q.sph, q.shapes, q);
+      else if (pl) hipLaunchKernelGGL((phong_kernel<true, true, false>), grid, dim3(kBlock), 0, stream, q.sph, q.shapes, q);
+      else if (lt) hipLaunchKernelGGL((phong_kernel<true, false, true>), grid, dim3(kBlock), ltb, stream, q.sph, q.shapes, q);
+      else hipLaunchKernelGGL((phong_kernel<true, false, false>), grid, dim3(kBlock), 0, stream, q.sph, q.shapes, q);
       break;
     case K_HYBRID:
       if (pl && lt) hipLaunchKernelGGL((hybrid_kernel<true, true, true, 0, kHyBW, kHyBW>), grid, hyb, ltb, stream, q.tile_order, q.sph, q.shapes, grid.x, q);

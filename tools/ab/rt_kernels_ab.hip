@@ -266,7 +266,7 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
   }
   if (ab_general() && (program == K_PHONG || program == K_HYBRID)) {
     const size_t lds = shapes_lds_bytes(p);
-    if (program == K_PHONG) hipLaunchKernelGGL((phong_kernel<false>), grid, dim3(kBlock), lds, stream, q);
+    if (program == K_PHONG) hipLaunchKernelGGL((phong_kernel<false>), grid, dim3(kBlock), lds, stream, q.sph, q.shapes, q);
     else hipLaunchKernelGGL((hybrid_kernel<false>), grid, dim3(kBlock), lds, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
     return hipGetLastError();
   }
