@@ -1253,6 +1253,13 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         float uw[2];
         grandom_n<2>({((s.x + px * f.z) - px) + f.x, s.z * px - (f.x * px) * f.z},
                      {((f.y + py * s.w) - py) + s.y, f.w * py - (s.y * py) * s.w}, uw);
+        if (ABL == 4) {  // instruction-budget ablation: the jitter hashes twice
+          float z, uw2[2];
+          asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+          grandom_n<2>({((s.x + px * f.z) - px) + f.x + z, s.z * px - (f.x * px) * f.z + z},
+                       {((f.y + py * s.w) - py) + s.y, f.w * py - (s.y * py) * s.w}, uw2);
+          if (__float_as_uint(uw2[0]) == 0x7fc00001u && __float_as_uint(uw2[1]) == 0x7fc00001u) uw[0] = uw2[0];
+        }
         float u = uw[0], w = uw[1];
         normalize2(u, w);
         const float jx = aa == 0 ? 0.0f : div_rn_by(u, 6.0f, kInv6) - 0.08333f;
@@ -1269,6 +1276,13 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         float abe[3];
         grandom_n<3>({f.x + px * s.z, f.z - px * s.z, s.x * px + s.z}, {f.y + py * s.w, f.w - py * s.w, s.y * py + s.w},
                      abe);
+        if (ABL == 4) {  // instruction-budget ablation: the hemisphere hashes twice
+          float z, abe2[3];
+          asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+          grandom_n<3>({f.x + px * s.z + z, f.z - px * s.z + z, s.x * px + s.z + z},
+                       {f.y + py * s.w, f.w - py * s.w, s.y * py + s.w}, abe2);
+          if (__float_as_uint(abe2[0]) == 0x7fc00001u && __float_as_uint(abe2[2]) == 0x7fc00001u) abe[1] = abe2[1];
+        }
         return normalize(mk(abe[0] * 2.0f - 1.0f, abe[1] * 2.0f - 1.0f, abe[2] * 2.0f - 1.0f));
       };
       if (!LAZY) bhemi = hemisphere();
@@ -1369,6 +1383,15 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
                 }
                 // the skip as a branch on the ballot (VCC), not an exec-mask save / restore per survivor
                 const bool pass = fmaf(bdir.z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w;
+                if (ABL == 5) {  // instruction-budget ablation: each survivor iteration twice
+                  float z, t2 = t;
+                  int i2 = ind;
+                  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+                  const bool pass2 = fmaf(bdir.z + z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w;
+                  if (__builtin_amdgcn_ballot_w64(pass2) != 0)
+                    sphere_candidate_if(mk(bpos.x + z, bpos.y, bpos.z), bdir, g, k, 0.0001f, t2, i2, pass2);
+                  if (i2 == 0x7fffffff) t = t2;
+                }
                 if (__builtin_amdgcn_ballot_w64(pass) != 0) sphere_candidate_if(bpos, bdir, g, k, 0.0001f, t, ind, pass);
               }
             if (ABL == 6) lap(6);
@@ -1570,6 +1593,16 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         if (has) {
           // (streaming the word's 4-sphere groups with a per-nibble skip, or loading 4 survivors
           // per wait, were slower: configs d / e +1.2% / +0% and +0% / +5%, r03f / r03i)
+          if (ABL == 1) {  // instruction-budget ablation: the cluster rounds' tests twice
+            float z, t2 = -1.0f;
+            int i2 = -1;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+            for (unsigned long long m2 = m; m2;) {
+              const int i = (w << 6) + pop_lowest(m2);
+              sphere_candidate(mk(pos.x + z, pos.y, pos.z), dir, geo[i], i, 0.0001f, t2, i2);
+            }
+            if (i2 == 0x7fffffff) t = t2;
+          }
           while (m) {
             const int i = (w << 6) + pop_lowest(m);
             sphere_candidate(pos, dir, geo[i], i, 0.0001f, t, ind);

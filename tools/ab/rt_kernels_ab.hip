@@ -193,7 +193,18 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true>), g, b, psh, stream, q, q.sph);
   else if (variant == 11)
     hipLaunchKernelGGL((ao_batch_kernel<7, false>), g, b, psh, stream, q, q.sph);
-  else if (variant == 91)
+  else if (variant >= 101 && variant <= 105 && tl && p.spp == 16 && p.nplanes == 0 && q.ncl > 0) {
+    // instruction budget (tools/sq_budget.sh): the production (d) instantiation (no counters,
+    // depth 20, clusters) and its ablations, each repeating one section's work once more:
+    // 101 none, 102 cluster-round tests (ABL 1), 103 culled primary tests (ABL 2), 104 the five
+    // hashes (ABL 4), 105 first-bounce survivor iterations (ABL 5)
+    const size_t ps = (size_t)batch_lds(16, kPool, p.nobj).total;
+    if (variant == 101) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
+    if (variant == 102) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 1, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
+    if (variant == 103) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
+    if (variant == 104) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 4, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
+    if (variant == 105) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 5, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
+  } else if (variant == 91)
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 1>), g, b, psh, stream, q, q.sph);
   else if (variant == 92)
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2>), g, b, psh, stream, q, q.sph);
