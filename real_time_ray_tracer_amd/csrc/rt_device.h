@@ -381,12 +381,16 @@ __device__ __forceinline__ void sphere_candidate(f3 pos, f3 dir, float4 g, int i
 // sphere_candidate for the lanes with `on` only (the others run the arithmetic and accept nothing):
 // callers branch on a wave-uniform ballot of `on` instead of masking exec per lane.
 __device__ __forceinline__ void sphere_candidate_if(f3 pos, f3 dir, float4 g, int i, float thr, float& t, int& ind,
-                                                    bool on) {
+                                                    unsigned long long onm) {
+  // onm: the lanes whose pre-test passed, as the wave mask (the caller's ballot).  Every
+  // decision stays a scalar mask: the branch on (del >= 0) & onm, and the acceptance mask that
+  // drives the two selects (VOP3 v_cndmask with an SGPR-pair mask).  With a per-lane bool
+  // argument the compiler rebuilt the mask through a v_cndmask + v_cmp pair per survivor.
   f3 pmc = pos - xyz(g);
   float b = dot(dir, pmc);
   float del = fmaf(g.w, g.w, fmaf(b, b, -dot(pmc, pmc)));
-  const bool hit = on & (del >= 0.0f);
-  if (__builtin_amdgcn_ballot_w64(hit) != 0) {
+  const unsigned long long hm = __builtin_amdgcn_ballot_w64(del >= 0.0f) & onm;
+  if (hm != 0) {
     // One straight-line tail for del == 0 and del > 0: with s = sqrt(0) = 0 both roots are
     // -b, so the reference's (del == 0 ? -b : root choice) differs only in values <= 0, and
     // (t2 < 0 ? t1 : t2) differs from (t2 < 0 ? (t1 < 0 ? -1 : t1) : t2) only when t1 < 0:
@@ -402,9 +406,14 @@ __device__ __forceinline__ void sphere_candidate_if(f3 pos, f3 dir, float4 g, in
     // (res < t || t < 0) as one unsigned compare: t is -1.0f (no hit yet, bits 0xBF800000, above
     // every positive float's bits, +inf included) or an accepted res > thr >= 0; for res > thr
     // (positive, not NaN) and positive t the float and bit orders agree
-    const bool acc = hit & (res > thr) & (__float_as_uint(res) < __float_as_uint(t));  // no short-circuit branches
-    t = acc ? res : t;
-    ind = acc ? i : ind;
+    const unsigned long long am = hm & __builtin_amdgcn_ballot_w64(res > thr) &
+                                  __builtin_amdgcn_ballot_w64(__float_as_uint(res) < __float_as_uint(t));
+    float tn;
+    int in;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(tn) : "v"(t), "v"(res), "s"(am));
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(in) : "v"(ind), "v"(i), "s"(am));
+    t = tn;
+    ind = in;
   }
 }
 

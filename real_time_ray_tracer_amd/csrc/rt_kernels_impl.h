@@ -1388,11 +1388,12 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
                   int i2 = ind;
                   asm volatile("v_mov_b32 %0, 0" : "=v"(z));
                   const bool pass2 = fmaf(bdir.z + z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w;
-                  if (__builtin_amdgcn_ballot_w64(pass2) != 0)
-                    sphere_candidate_if(mk(bpos.x + z, bpos.y, bpos.z), bdir, g, k, 0.0001f, t2, i2, pass2);
+                  const unsigned long long pm2 = __builtin_amdgcn_ballot_w64(pass2);
+                  if (pm2 != 0) sphere_candidate_if(mk(bpos.x + z, bpos.y, bpos.z), bdir, g, k, 0.0001f, t2, i2, pm2);
                   if (i2 == 0x7fffffff) t = t2;
                 }
-                if (__builtin_amdgcn_ballot_w64(pass) != 0) sphere_candidate_if(bpos, bdir, g, k, 0.0001f, t, ind, pass);
+                const unsigned long long pm = __builtin_amdgcn_ballot_w64(pass);
+                if (pm != 0) sphere_candidate_if(bpos, bdir, g, k, 0.0001f, t, ind, pm);
               }
             if (ABL == 6) lap(6);
           } else if (live) {
