@@ -1,0 +1,18 @@
+#!/usr/bin/env bash
+# round 5u: non-temporal colour stores (build/v_nts, RT_NT_STORE=1) vs production: hybrid (b),
+# phong (a) bursts, AO (d) per launch, and the driver's (d) command (AO + post-process) alternating
+set -uo pipefail
+O=gpurun_out/r05u
+mkdir -p $O
+L=real_time_ray_tracer_amd/librtrt.so,build/v_nts/librtrt.so
+timeout -k 10 300 python -u tools/explore/r05/hybrid_burst.py --libs $L --rounds 5 > $O/hybrid_b.txt 2>&1 &&
+timeout -k 10 300 python -u tools/explore/r05/hybrid_burst.py --config a --libs $L --rounds 5 > $O/phong_a.txt 2>&1 &&
+timeout -k 10 300 python -u tools/ab.py --config d --libs $L --rounds 5 --frames 4 > $O/ab_d.txt 2>&1 &&
+for i in 1 2; do
+  timeout -k 10 200 python -u bench.py --no-cpu-baseline > $O/bench_d_prod_$i.json 2> $O/bench_d_prod_$i.err &&
+  RTRT_LIB=build/v_nts/librtrt.so timeout -k 10 200 python -u bench.py --no-cpu-baseline > $O/bench_d_nts_$i.json 2> $O/bench_d_nts_$i.err || exit 1
+done
+rc=$?
+tail -1 $O/hybrid_b.txt; tail -1 $O/phong_a.txt; tail -1 $O/ab_d.txt
+for f in $O/bench_d_*.json; do python3 -c "import json; d=json.load(open('$f')); print('$f', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d.get('roofline_post',{}).get('kernel_ms'))"; done
+exit $rc
