@@ -277,8 +277,12 @@ enum {
   RT_MATH_SQRT_TAIL_SWEEP = 8, /* out[i] = #bit patterns in [i*in[0], (i+1)*in[0]) of the finite
                              non-negative floats where the hit-tail sqrt breaks its contract
                              (== sqrtf on [2^-96, FLT_MAX], in [0, 2^-47] below)          */
-  RT_MATH_SIN_RANGE = 9   /* out[i] = sin(x) of random() for the float whose bit pattern is
+  RT_MATH_SIN_RANGE = 9,  /* out[i] = sin(x) of random() for the float whose bit pattern is
                              bits(in[0]) + i (mod 2^32): exhaustive sweeps without inputs  */
+  RT_MATH_SHADOW = 10     /* shadow_ray's occluder test (p_compute.glsl:159-161) as the
+                             kernels decide it: in = (light - pos).xyz, t quads; l =
+                             normalize(light - pos), len = length(light - pos); out = (l.xyz,
+                             len, 1 if t > 0.0001 && length(dvec3(t * l)) < len else 0)     */
 };
 int rt_selftest_math(rt_ctx* ctx, int fn, const float* in, float* out, size_t n);
 

@@ -21,7 +21,7 @@ RT_PROG_P_COMPUTE = 4
 RT_PROG_H_COMPUTE = 5
 RT_MODE_AO_PP, RT_MODE_AO, RT_MODE_PHONG, RT_MODE_PHONG_REFL = 1, 2, 3, 4
 (RT_MATH_SIN, RT_MATH_RANDOM, RT_MATH_SQRT, RT_MATH_DIV, RT_MATH_NORMALIZE, RT_MATH_SPHERE, RT_MATH_SQRT_SWEEP,
- RT_MATH_RCP_SWEEP, RT_MATH_SQRT_TAIL_SWEEP, RT_MATH_SIN_RANGE) = range(10)
+ RT_MATH_RCP_SWEEP, RT_MATH_SQRT_TAIL_SWEEP, RT_MATH_SIN_RANGE, RT_MATH_SHADOW) = range(11)
 RT_NUM_FRAMES = 8
 RT_RECURSION_DEPTH = 20
 RT_SHAPE_SPHERE, RT_SHAPE_RECTANGLE, RT_SHAPE_PLANE = 1, 3, 5

@@ -225,8 +225,12 @@ struct FrameDst {
   float4* out_pix;
   float4* image;
 };
+// MF = false: a single-frame launch (mf_n = 0, the host's choice): the frame's light and
+// destinations come straight from the kernel arguments, with no branch on mf_n, so a wave's
+// first scalar loads issue together instead of one dependent round trip after another
+template <bool MF = true>
 __device__ __forceinline__ FrameDst frame_dst(const FrameParams& P, int j) {
-  if (P.mf_n <= 0) return FrameDst{mk(P.Lx, P.Ly, P.Lz), P.out_pix, P.image};
+  if (!MF || P.mf_n <= 0) return FrameDst{mk(P.Lx, P.Ly, P.Lz), P.out_pix, P.image};
   const float4 L = P.mf_light[j];
   return FrameDst{mk(L.x, L.y, L.z), (float4*)P.hist_pix[(P.mf_slot0 + j) % P.F], j == P.mf_n - 1 ? P.image : nullptr};
 }
@@ -541,10 +545,28 @@ __device__ __forceinline__ ConeF wave_tile_cone(const FrameParams& P, int bx, in
 // rest are tested as shadow_lit does.  "Some occluder exists" does not depend on the order.
 // Must be called by every lane of the wave (ballots and shuffles).
 constexpr int kShadowConeMinObj = 8;
-// the binary64 occluder test of shadow_ray (p_compute.glsl:155-163) for one object's float t
-__device__ __forceinline__ bool shadow_occludes(float tf, f3 l, double dlen) {
+// the binary64 occluder test of shadow_ray (p_compute.glsl:155-163) for one object's float t:
+// t > 0.0001 and length(dvec3(t * l)) < len.  With |l| within 2^-18.8 of 1 (checked per ray, see
+// shadow_bounds) the binary64 length is t |l| (1 +- 2^-51), so t < len (1 - 2^-12) and
+// t > len (1 + 2^-12) (float products, each within 2^-24) decide the test exactly; only t within
+// 2^-12 of len (an occluder at the light's distance) runs the binary64 sequence.
+// (RT_SHADOW_FAST=0: the binary64 sequence for every t, A/B builds)
+#ifndef RT_SHADOW_FAST
+#define RT_SHADOW_FAST 0
+#endif
+struct ShadowBounds {
+  float lo, hi;  // t < lo: occludes; t > hi: does not (finite bounds only when |l|^2 is within 2^-19 of 1)
+};
+__device__ __forceinline__ ShadowBounds shadow_bounds(f3 l, float len) {
+  const float l2 = dot(l, l);  // within 3 ulps of |l|^2
+  const bool ok = RT_SHADOW_FAST && fabsf(l2 - 1.0f) < 0x1p-19f;
+  return ok ? ShadowBounds{len * (1.0f - 0x1p-12f), len * (1.0f + 0x1p-12f)} : ShadowBounds{0.0f, INFINITY};
+}
+__device__ __forceinline__ bool shadow_occludes(float tf, f3 l, double dlen, ShadowBounds sb) {
+  if (!(tf > 0.0001f)) return false;  // (double)tf > (double)0.0001f, exactly
+  if (tf < sb.lo) return true;
+  if (tf > sb.hi) return false;
   const double t = (double)tf;
-  if (!(t > (double)0.0001f)) return false;
   const double dx = t * (double)l.x, dy = t * (double)l.y, dz = t * (double)l.z;
   return sqrt(fma(dz, dz, fma(dy, dy, dx * dx))) < dlen;
 }
@@ -558,14 +580,15 @@ __device__ __forceinline__ bool shadow_lit_cone(const FrameParams& P, const floa
   const float len = sqrtf(dot(lv, lv));
   const f3 np = pos + 0.01f * l;
   const double dlen = (double)len;
+  const ShadowBounds sb = shadow_bounds(l, len);
   if (__ballot(need) == 0) return true;
   bool lit = true;
   if (PL)
     for (int k = 0; k < P.nplanes; ++k)
-      if (need && lit && shadow_occludes(plane_eval(np, l, P.planes[2 * k], P.planes[2 * k + 1]), l, dlen)) lit = false;
+      if (need && lit && shadow_occludes(plane_eval(np, l, P.planes[2 * k], P.planes[2 * k + 1]), l, dlen, sb)) lit = false;
   if (n <= kShadowConeMinObj) {  // small scenes: the cone costs more than it saves
     for (int k = 0; k < n; ++k) {
-      if (need && lit && shadow_occludes(sphere_eval_shadow(np, l, geo[k]), l, dlen)) lit = false;
+      if (need && lit && shadow_occludes(sphere_eval_shadow(np, l, geo[k]), l, dlen, sb)) lit = false;
     }
     return lit;
   }
@@ -593,7 +616,7 @@ __device__ __forceinline__ bool shadow_lit_cone(const FrameParams& P, const floa
     while (m) {
       const int k = w + __builtin_ctzll(m);
       m &= m - 1;
-      if (need && lit && shadow_occludes(sphere_eval_shadow(np, l, geo[k]), l, dlen)) lit = false;
+      if (need && lit && shadow_occludes(sphere_eval_shadow(np, l, geo[k]), l, dlen, sb)) lit = false;
     }
   }
   return lit;
@@ -612,11 +635,12 @@ __device__ __forceinline__ bool shadow_lit_sph(const FrameParams& P, const float
   const float len = sqrtf(dot(lv, lv));
   const f3 np = pos + 0.01f * l;
   const double dlen = (double)len;
+  const ShadowBounds sb = shadow_bounds(l, len);
   if (PL)
     for (int k = 0; k < P.nplanes; ++k)
-      if (shadow_occludes(plane_eval(np, l, P.planes[2 * k], P.planes[2 * k + 1]), l, dlen)) return false;
+      if (shadow_occludes(plane_eval(np, l, P.planes[2 * k], P.planes[2 * k + 1]), l, dlen, sb)) return false;
   for (int i = 0; i < n; ++i)
-    if (shadow_occludes(sphere_eval_shadow(np, l, geo[i]), l, dlen)) return false;
+    if (shadow_occludes(sphere_eval_shadow(np, l, geo[i]), l, dlen, sb)) return false;
   return true;
 }
 
@@ -688,7 +712,7 @@ __device__ __forceinline__ void stage_tables(const FrameParams& P, float4* lds) 
 }
 
 // (the sphere and shape tables lead the arguments: preloaded into SGPRs, as for hybrid_kernel)
-template <bool ALLSPH, bool PL = false, bool LT = false>
+template <bool ALLSPH, bool PL = false, bool LT = false, bool MF = true>
 __global__ __launch_bounds__(kBlock) void phong_kernel(const float4* __restrict__ gsph, const float4* __restrict__ gshp,
                                                        FrameParams P) {
   extern __shared__ float4 lds[];
@@ -696,6 +720,10 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(const float4* __restrict_
     if (LT) stage_tables(P, lds);
     else stage_shapes(P, lds);
     __syncthreads();
+  }
+  if constexpr (!MF) {  // single-frame launch (frame_dst<false>)
+    phong_tile<ALLSPH, PL, LT>(P, lds, blockIdx.x, blockIdx.y, frame_dst<false>(P, 0), gsph, gshp);
+    return;
   }
   int j0;
   const int nj = block_frames<kPhongFramesPerBlock>(P, j0);
@@ -769,10 +797,11 @@ __device__ __forceinline__ void bounce_round(const FrameParams& P, const float4*
     const float len = sqrtf(dot(lv, lv));
     const f3 np = curr + 0.01f * l;
     const double dlen = (double)len;
+    const ShadowBounds sb = shadow_bounds(l, len);
     if (PL)
       for (int k = pl; k < P.nplanes && !occ; k += G)
-        occ = shadow_occludes(plane_eval(np, l, P.planes[2 * k], P.planes[2 * k + 1]), l, dlen);
-    for (int i = pl; i < n && !occ; i += G) occ = shadow_occludes(sphere_eval_shadow(np, l, geo[i]), l, dlen);
+        occ = shadow_occludes(plane_eval(np, l, P.planes[2 * k], P.planes[2 * k + 1]), l, dlen, sb);
+    for (int i = pl; i < n && !occ; i += G) occ = shadow_occludes(sphere_eval_shadow(np, l, geo[i]), l, dlen, sb);
   }
   unsigned oc = occ ? 1u : 0u;
   for (int m = 1; m < G; m <<= 1) oc |= (unsigned)__shfl_xor((int)oc, m);
@@ -906,7 +935,7 @@ __device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* 
 // preloads the first kernel arguments into SGPRs (-mllvm -amdgpu-kernarg-preload-count, Makefile),
 // so a wave's first loads (its tile, then the culls' sphere rows) need not wait for a kernarg load.
 // (FrameParams, an aggregate, is never preloaded.)
-template <bool ALLSPH, bool PL = false, bool LT = false, int ABL = 0, int BWX = 2, int BWY = 2>
+template <bool ALLSPH, bool PL = false, bool LT = false, int ABL = 0, int BWX = 2, int BWY = 2, bool MF = true>
 __global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(const unsigned* __restrict__ tord,
                                                                 const float4* __restrict__ gsph,
                                                                 const float4* __restrict__ gshp, unsigned gx,
@@ -953,7 +982,7 @@ __global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(const unsigned* 
       by = t >> 16;
     }
     hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), bx, by,
-                                               frame_dst(P, blockIdx.z), gsph, gshp);
+                                               frame_dst<MF>(P, blockIdx.z), gsph, gshp);
   } else {
     int j0;
     const int nj = block_frames<kHybridFramesPerBlock>(P, j0);
@@ -2004,6 +2033,15 @@ __global__ void selftest_kernel(int fn, const float* __restrict__ in, float* __r
       break;
     }
     case 3: out[i] = in[2 * i] / in[2 * i + 1]; break;
+    case 10: {  // shadow_lit_cone's per-ray set-up and occluder test for one (light - pos, t)
+      const f3 lv = mk(in[4 * i], in[4 * i + 1], in[4 * i + 2]);
+      const f3 l = normalize(lv);
+      const float len = sqrtf(dot(lv, lv));
+      const bool occ = shadow_occludes(in[4 * i + 3], l, (double)len, shadow_bounds(l, len));
+      out[5 * i] = l.x; out[5 * i + 1] = l.y; out[5 * i + 2] = l.z; out[5 * i + 3] = len;
+      out[5 * i + 4] = occ ? 1.0f : 0.0f;
+      break;
+    }
     case 4: {
       f3 v = normalize(mk(in[3 * i], in[3 * i + 1], in[3 * i + 2]));
       out[3 * i] = v.x; out[3 * i + 1] = v.y; out[3 * i + 2] = v.z;
@@ -2168,18 +2206,23 @@ inline hipError_t launch_production(int program, const FrameParams& p, const Fra
 #endif
   const bool lt = p.nobj <= kTabLdsMax && !(RT_HY_NOLT && program == K_HYBRID) && !(RT_PH_NOLT && program == K_PHONG);
   const size_t ltb = lt ? tab_lds_bytes(p) : 0;
+  const bool mf = p.mf_n > 0;  // multi-frame launch; single-frame ones take the MF = false kernels
   switch (program) {
     case K_PHONG:
       if (pl && lt) hipLaunchKernelGGL((phong_kernel<true, true, true>), grid, dim3(kBlock), ltb, stream, q.sph, q.shapes, q);
-      else if (pl) hipLaunchKernelGGL((phong_kernel<true, true, false>), grid, dim3(kBlock), 0, stream, q.sph, q.shapes, q);
+      else if (pl && mf) hipLaunchKernelGGL((phong_kernel<true, true, false>), grid, dim3(kBlock), 0, stream, q.sph, q.shapes, q);
+      else if (pl) hipLaunchKernelGGL((phong_kernel<true, true, false, false>), grid, dim3(kBlock), 0, stream, q.sph, q.shapes, q);
       else if (lt) hipLaunchKernelGGL((phong_kernel<true, false, true>), grid, dim3(kBlock), ltb, stream, q.sph, q.shapes, q);
-      else hipLaunchKernelGGL((phong_kernel<true, false, false>), grid, dim3(kBlock), 0, stream, q.sph, q.shapes, q);
+      else if (mf) hipLaunchKernelGGL((phong_kernel<true, false, false>), grid, dim3(kBlock), 0, stream, q.sph, q.shapes, q);
+      else hipLaunchKernelGGL((phong_kernel<true, false, false, false>), grid, dim3(kBlock), 0, stream, q.sph, q.shapes, q);
       break;
     case K_HYBRID:
       if (pl && lt) hipLaunchKernelGGL((hybrid_kernel<true, true, true, 0, kHyBW, kHyBW>), grid, hyb, ltb, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
-      else if (pl) hipLaunchKernelGGL((hybrid_kernel<true, true, false, 0, kHyBW, kHyBW>), grid, hyb, 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+      else if (pl && mf) hipLaunchKernelGGL((hybrid_kernel<true, true, false, 0, kHyBW, kHyBW>), grid, hyb, 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+      else if (pl) hipLaunchKernelGGL((hybrid_kernel<true, true, false, 0, kHyBW, kHyBW, false>), grid, hyb, 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
       else if (lt) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 0, kHyBW, kHyBW>), grid, hyb, ltb, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
-      else hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, kHyBW, kHyBW>), grid, hyb, 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+      else if (mf) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, kHyBW, kHyBW>), grid, hyb, 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+      else hipLaunchKernelGGL((hybrid_kernel<true, false, false, 0, kHyBW, kHyBW, false>), grid, hyb, 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
       break;
     case K_POST:
       hipLaunchKernelGGL(post_kernel,

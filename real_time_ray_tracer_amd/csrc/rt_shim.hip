@@ -1518,8 +1518,8 @@ int rt_read_row_counters(rt_ctx* c, uint64_t* rows, int reset) {
 }
 
 int rt_selftest_math(rt_ctx* c, int fn, const float* in, float* out, size_t n) {
-  if (!c || !in || !out || fn < 0 || fn > RT_MATH_SIN_RANGE) return RT_E_INVAL;
-  static const int in_w[] = {1, 2, 1, 2, 3, 10, 0, 0, 0, 0}, out_w[] = {1, 1, 1, 1, 3, 1, 1, 1, 1, 1};
+  if (!c || !in || !out || fn < 0 || fn > RT_MATH_SHADOW) return RT_E_INVAL;
+  static const int in_w[] = {1, 2, 1, 2, 3, 10, 0, 0, 0, 0, 4}, out_w[] = {1, 1, 1, 1, 3, 1, 1, 1, 1, 1, 5};
   RT_HIP(c, hipSetDevice(c->device));
   float *din = nullptr, *dout = nullptr;
   const bool sweep = fn == RT_MATH_SQRT_SWEEP || fn == RT_MATH_RCP_SWEEP || fn == RT_MATH_SQRT_TAIL_SWEEP ||

@@ -346,8 +346,14 @@ class Renderer:
         return out
 
     def selftest_math(self, fn: int, inputs: np.ndarray, n: int) -> np.ndarray:
-        out_w = {_lib.RT_MATH_NORMALIZE: 3}.get(fn, 1)
+        out_w = {_lib.RT_MATH_NORMALIZE: 3, _lib.RT_MATH_SHADOW: 5}.get(fn, 1)
+        in_w = {_lib.RT_MATH_RANDOM: 2, _lib.RT_MATH_DIV: 2, _lib.RT_MATH_NORMALIZE: 3, _lib.RT_MATH_SPHERE: 10,
+                _lib.RT_MATH_SHADOW: 4}.get(fn, 1)
         inp = np.ascontiguousarray(inputs, np.float32).reshape(-1)
+        sweep = fn in (_lib.RT_MATH_SQRT_SWEEP, _lib.RT_MATH_RCP_SWEEP, _lib.RT_MATH_SQRT_TAIL_SWEEP,
+                       _lib.RT_MATH_SIN_RANGE)
+        if inp.size < (1 if sweep else n * in_w):
+            raise ValueError(f"selftest_math: {inp.size} input floats for n = {n} (need {1 if sweep else n * in_w})")
         out = np.empty(n * out_w, np.float32)
         self._c(self._lib.rt_selftest_math(self.ctx, fn, fptr(inp), fptr(out), n), "rt_selftest_math")
         return out

@@ -316,6 +316,67 @@ def test_math_primitives_bitwise():
     r.close()
 
 
+def _shadow_occludes_b64(l, ln, t):
+    """shadow_ray's occluder test in binary64 (p_compute.glsl:159-161, the oracle's
+    rto_shadow sequence): t > 0.0001 and sqrt(fma(dz, dz, fma(dy, dy, dx * dx))) < len with
+    d = t * l; each fma rounded once, by exact rationals."""
+    from fractions import Fraction as Fr
+    import math
+    t = float(t)
+    if not t > float(np.float32(0.0001)):
+        return False
+    dx, dy, dz = t * float(l[0]), t * float(l[1]), t * float(l[2])
+
+    def fma(a, b, c):
+        if not (math.isfinite(a) and math.isfinite(b) and math.isfinite(c)):
+            return a * b + c
+        return float(Fr(a) * Fr(b) + Fr(c))
+    q = fma(dz, dz, fma(dy, dy, dx * dx))
+    return (math.sqrt(q) if q >= 0 else math.nan) < float(ln)
+
+
+def test_shadow_occluder_decision():
+    """The kernels decide most shadow occluder tests in float (t against len (1 -+ 2^-12)) and
+    run the binary64 sequence only near len: the decision equals the binary64 one on t drawn at
+    and around both bounds, around len itself (where only the binary64 sequence decides), and
+    for degenerate light vectors (zero, tiny, huge: the float bounds are off there)."""
+    r = Renderer(8, 8, 1, 1)
+    rng = np.random.default_rng(11)
+    n = 6000
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    lv = (d * 10.0 ** rng.uniform(-2, 3.5, (n, 1))).astype(np.float32)
+    lv = np.concatenate([lv, np.array([[0, 0, 0], [1e-25, 2e-25, 0], [3e-20, 0, 1e-20], [1e25, 1e25, 0],
+                                       [3e38, 3e38, 0], [np.nan, 0, 0], [np.inf, 1, 0]], np.float32)])
+    m = len(lv)
+    probe = r.selftest_math(_lib.RT_MATH_SHADOW, np.concatenate([lv, np.ones((m, 1), np.float32)], 1), m)
+    ln = probe.reshape(m, 5)[:, 3]
+    # t per light vector: both bounds and len itself, each -+ a few ulps, plus random and special values
+    ts = []
+    for f in (1 - 2.0 ** -12, 1 + 2.0 ** -12, 1.0, 1 - 2.0 ** -20, 1 + 2.0 ** -20):
+        base = (ln.astype(np.float64) * f).astype(np.float32)
+        for k in (-3, -1, 0, 1, 3):
+            ts.append(np.nextafter(base, np.float32(np.inf) if k > 0 else np.float32(-np.inf)) if k else base)
+            for _ in range(abs(k) - 1):
+                ts[-1] = np.nextafter(ts[-1], np.float32(np.inf) if k > 0 else np.float32(-np.inf))
+    ts.append((ln * rng.uniform(0, 2, m)).astype(np.float32))
+    ts.append(np.full(m, np.float32(0.0001)))
+    ts.append(np.full(m, np.nextafter(np.float32(0.0001), np.float32(1))))
+    for v in (-1.0, np.inf, np.nan):
+        ts.append(np.full(m, v, np.float32))
+    T = np.stack(ts, 1).astype(np.float32)  # [m, k]
+    k = T.shape[1]
+    inp = np.concatenate([np.repeat(lv, k, 0), T.reshape(-1, 1)], 1)
+    out = r.selftest_math(_lib.RT_MATH_SHADOW, inp, len(inp)).reshape(-1, 5)
+    r.close()
+    got = out[:, 4] == 1.0
+    want = np.array([_shadow_occludes_b64(o[:3], o[3], t) for o, t in zip(out, inp[:, 3])])
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, f"{bad.size} of {len(inp)} decisions differ; first: lv={inp[bad[0], :3]} t={inp[bad[0], 3]!r} " \
+                          f"len={out[bad[0], 3]!r} kernel={got[bad[0]]} binary64={want[bad[0]]}"
+    assert want.any() and (~want).any()
+
+
 def test_sqrt_rn_exhaustive():
     """The kernels' explicit sqrt sequence equals sqrtf on every non-negative float
     (0 .. +inf: 2^31 - 2^23 + 1 bit patterns), on the device."""

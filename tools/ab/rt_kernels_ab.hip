@@ -242,18 +242,18 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
   dim3 grid((p.W + 15) / 16, (p.trace_rows + 15) / 16, p.mf_n > 0 ? (p.mf_n + fpb - 1) / fpb : 1);
   if (const char* ea = getenv("RTRT_HY_ABL"); ea && program == K_HYBRID && !pl && atoi(ea) > 0) {
     const int a = atoi(ea);
-    const size_t lt = tab_lds_bytes(p);
+    const size_t lt = tab_lds_bytes(p);  // (7: LDS tables, 8: production tables through the caches)
     if (kHyBW != 2) {  // 2x2 blocks here; the schedule's tables are sized for the production blocks
       q.tile_order = nullptr;
       q.tile_cost = nullptr;
     }
-    if (a == 1) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 1>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
-    else if (a == 3) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 3>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
-    else if (a == 5) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 5>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
-    else if (a == 6) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 6>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+    if (a == 1) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 1>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+    else if (a == 3) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 3>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+    else if (a == 5) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 5>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+    else if (a == 6) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 6>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
     else if (a == 7) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 7>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
     else if (a == 8) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 7>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
-    else hipLaunchKernelGGL((hybrid_kernel<true, false, true, 2>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+    else hipLaunchKernelGGL((hybrid_kernel<true, false, false, 2>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
     return hipGetLastError();
   }
   if (const char* eb = getenv("RTRT_HY_BLK"); eb && program == K_HYBRID && !pl) {  // block shape A/B
