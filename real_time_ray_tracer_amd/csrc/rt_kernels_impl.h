@@ -511,19 +511,27 @@ __device__ __forceinline__ unsigned long long plane_cone_mask(const FrameParams&
 // SKIP (timing ablation): cull only, no tests.
 template <bool PL, bool SKIP = false>
 __device__ __forceinline__ int closest_hit_cone(const FrameParams& P, const float4* __restrict__ geo, int nobj,
-                                                const ConeF& cone, f3 cam, f3 dir, float thr, float& t_out) {
+                                                const ConeF& cone, f3 cam, f3 dir, float thr, float& t_out,
+                                                const float4* pre0 = nullptr) {
   float t = -1.0f;
   int ind = -1;
   const int lane = threadIdx.x & 63;
-  for (int w = 0; w < nobj; w += 64) {
-    const int i = w + lane;
-    const bool keep = i < nobj && !cone_misses_f(cone, geo[i], cam.x, cam.y, cam.z);
+  auto word = [&](int w, bool keep) {
     unsigned long long m = uniform_mask(__ballot(keep));
     while (m && !SKIP) {
       const int k = w + __builtin_ctzll(m);
       m &= m - 1;
       sphere_candidate(cam, dir, geo[k], k, thr, t, ind);
     }
+  };
+  int w = 0;
+  if (pre0 && nobj > 0) {  // the first word's rows, already requested by the caller
+    word(0, lane < nobj && !cone_misses_f(cone, *pre0, cam.x, cam.y, cam.z));
+    w = 64;
+  }
+  for (; w < nobj; w += 64) {
+    const int i = w + lane;
+    word(w, i < nobj && !cone_misses_f(cone, geo[i], cam.x, cam.y, cam.z));
   }
   if (PL) plane_pass_masked(P, plane_cone_mask(P, cone, cam), cam, dir, thr, t, ind);
   t_out = t;
@@ -574,7 +582,7 @@ __device__ __forceinline__ bool shadow_occludes(float tf, f3 l, double dlen, Sha
 // spheres ("some occluder exists" does not depend on the order).
 template <bool PL>
 __device__ __forceinline__ bool shadow_lit_cone(const FrameParams& P, const float4* __restrict__ geo, int n, f3 light,
-                                                f3 pos, bool need) {
+                                                f3 pos, bool need, const float4* pre0 = nullptr) {
   const f3 lv = light - pos;
   const f3 l = normalize(lv);
   const float len = sqrtf(dot(lv, lv));
@@ -605,19 +613,25 @@ __device__ __forceinline__ bool shadow_lit_cone(const FrameParams& P, const floa
   cone.st = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - cd * cd));
   const bool wide = !(cd > 0.05f);  // nearly a half-space: test everything
   const int lane = threadIdx.x & 63;
-  for (int w = 0; w < n; w += 64) {
-    const int i = w + lane;
-    bool keep = i < n;
-    if (keep && !wide) {
-      const float4 g = geo[i];
-      keep = !cone_misses_f(cone, make_float4(g.x, g.y, g.z, g.w + 1e-4f), light.x, light.y, light.z);
-    }
+  auto word = [&](int w, bool keep) {
     unsigned long long m = uniform_mask(__ballot(keep));
     while (m) {
       const int k = w + __builtin_ctzll(m);
       m &= m - 1;
       if (need && lit && shadow_occludes(sphere_eval_shadow(np, l, geo[k]), l, dlen, sb)) lit = false;
     }
+  };
+  auto keep_row = [&](float4 g) {
+    return wide || !cone_misses_f(cone, make_float4(g.x, g.y, g.z, g.w + 1e-4f), light.x, light.y, light.z);
+  };
+  int w = 0;
+  if (pre0) {  // the first word's rows, already requested by the caller (n > kShadowConeMinObj here)
+    word(0, lane < n && keep_row(*pre0));
+    w = 64;
+  }
+  for (; w < n; w += 64) {
+    const int i = w + lane;
+    word(w, i < n && keep_row(geo[i]));
   }
   return lit;
 }
@@ -651,7 +665,8 @@ __device__ __forceinline__ bool shadow_lit_sph(const FrameParams& P, const float
 // tested through eval_ray's id dispatch, no culling.
 template <bool ALLSPH, bool PL, bool LT, int BWX = 2, int BWY = 2>
 __device__ __forceinline__ void phong_tile(const FrameParams& P, const float4* lds, int bx, int by, const FrameDst& fd,
-                                           const float4* __restrict__ gsph, const float4* __restrict__ gshp) {
+                                           const float4* __restrict__ gsph, const float4* __restrict__ gshp,
+                                           const float4* pre0 = nullptr) {
   const int n = P.nobj;
   const float4* tab = (ALLSPH && !LT) ? gshp : lds;                       // geo | geo2 | col
   const float4* geo = (ALLSPH && !LT) ? gsph : (ALLSPH ? lds + 4 * n : lds);  // what the sphere tests read
@@ -666,14 +681,14 @@ __device__ __forceinline__ void phong_tile(const FrameParams& P, const float4* l
   int ind;
   if (ALLSPH) {
     const ConeF cone = wave_tile_cone<BWX, BWY>(P, bx, by);
-    ind = closest_hit_cone<PL>(P, geo, n, cone, cam, dir, 0.0f, t);
+    ind = closest_hit_cone<PL>(P, geo, n, cone, cam, dir, 0.0f, t, pre0);
   } else {
     ind = closest_hit<ALLSPH>(geo, geo2, n, cam, dir, 0.0f, t);
   }
   count_work(P, active, y, 1u, active && ind != -1 ? 1u : 0u);
   const bool need = active && ind != -1;
   bool lit_w = true;
-  if (ALLSPH) lit_w = shadow_lit_cone<PL>(P, geo, n, light, cam + t * dir, need);  // every lane takes part
+  if (ALLSPH) lit_w = shadow_lit_cone<PL>(P, geo, n, light, cam + t * dir, need, pre0);  // every lane takes part
   if (!active) return;
   float r, g, b;
   if (ind == -1) {
@@ -722,7 +737,11 @@ __global__ __launch_bounds__(kBlock) void phong_kernel(const float4* __restrict_
     __syncthreads();
   }
   if constexpr (!MF) {  // single-frame launch (frame_dst<false>)
-    phong_tile<ALLSPH, PL, LT>(P, lds, blockIdx.x, blockIdx.y, frame_dst<false>(P, 0), gsph, gshp);
+    // the lane's row of the first 64-sphere word, requested before anything else (in bounds for
+    // any scene: the sphere table is followed by >= 64 rows of other tables, rt_kernels.h)
+    const float4 g0 = gsph[threadIdx.x & 63];
+    phong_tile<ALLSPH, PL, LT>(P, lds, blockIdx.x, blockIdx.y, frame_dst<false>(P, 0), gsph, gshp,
+                               (ALLSPH && !LT) ? &g0 : nullptr);
     return;
   }
   int j0;
@@ -816,7 +835,7 @@ __device__ __forceinline__ void bounce_round(const FrameParams& P, const float4*
 template <bool ALLSPH, bool PL, bool LT, int ABL = 0, int BWX = 2, int BWY = 2>
 __device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* lds, int* perm, int bx, int by,
                                             const FrameDst& fd, const float4* __restrict__ gsph,
-                                            const float4* __restrict__ gshp) {
+                                            const float4* __restrict__ gshp, const float4* pre0 = nullptr) {
   const int n = P.nobj;  // !ALLSPH or LT: LDS tables (see phong_kernel)
   const float4* tab = (ALLSPH && !LT) ? gshp : lds;
   const float4* geo = (ALLSPH && !LT) ? gsph : (ALLSPH ? lds + 4 * n : lds);
@@ -886,8 +905,8 @@ __device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* 
     int ind0 = -1;
     bool lit0 = true;
     const ConeF cone = wave_tile_cone<BWX, BWY>(P, bx, by);
-    if (ABL != 2) ind0 = closest_hit_cone<PL, ABL == 3>(P, geo, n, cone, pos, dir, 0.001f, t0);
-    if (ABL == 0 || ABL >= 4) lit0 = shadow_lit_cone<PL>(P, geo, n, light, pos + t0 * dir, active && ind0 != -1);  // every lane takes part
+    if (ABL != 2) ind0 = closest_hit_cone<PL, ABL == 3>(P, geo, n, cone, pos, dir, 0.001f, t0, pre0);
+    if (ABL == 0 || ABL >= 4) lit0 = shadow_lit_cone<PL>(P, geo, n, light, pos + t0 * dir, active && ind0 != -1, pre0);  // every lane takes part
     bool live = active && !segment(0, t0, ind0, lit0);
     // segments 1 .. D-1: bounce rounds with the whole wave
     int rounds = 0;  // wave-uniform: the wave's cost beyond its camera rays (tile schedule)
@@ -975,6 +994,11 @@ __global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(const unsigned* 
     // few tiles whose mirror paths bounce for many rounds start early instead of setting the
     // launch's tail (config (b): 32.0 -> 25.4 us per frame with the reverse of row order, which
     // happens to put that scene's bouncing tiles first)
+    // MF = false: the lane's row of the first 64-sphere word requested before the tile order (in
+    // bounds for any scene: the sphere table is followed by >= 64 rows of other tables)
+    const bool pre = !MF && ALLSPH && !LT;
+    float4 g0;
+    if (pre) g0 = gsph[threadIdx.x & 63];
     unsigned bx = blockIdx.x, by = blockIdx.y;
     if (tord) {
       const unsigned t = tord[blockIdx.x + blockIdx.y * gx];  // (gx = gridDim.x, a preloaded argument)
@@ -982,7 +1006,7 @@ __global__ __launch_bounds__(64 * BWX * BWY) void hybrid_kernel(const unsigned* 
       by = t >> 16;
     }
     hybrid_tile<ALLSPH, PL, LT, ABL, BWX, BWY>(P, lds, hperm + 64 * (threadIdx.x >> 6), bx, by,
-                                               frame_dst<MF>(P, blockIdx.z), gsph, gshp);
+                                               frame_dst<MF>(P, blockIdx.z), gsph, gshp, pre ? &g0 : nullptr);
   } else {
     int j0;
     const int nj = block_frames<kHybridFramesPerBlock>(P, j0);
