@@ -1062,6 +1062,12 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
 #ifndef RT_AO_MINW
 #define RT_AO_MINW 7
 #endif
+// the batched first bounce's exact tests deferred and merged over survivors with disjoint
+// pre-test masks (see the survivor loop): (d) 2.439 -> 2.414 ms, (c) 0.738 -> 0.730 ms
+// (profiles/r05z3_*); 0 = one exact pass per survivor that some lane passes (A/B builds)
+#ifndef RT_B1_DEFER
+#define RT_B1_DEFER 1
+#endif
 constexpr int kAoMinWaves = RT_AO_MINW;
 template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
           int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false, bool CL = true, int DC = 0,
@@ -1416,6 +1422,20 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         float t = -1.0f;
         int ind = -1;
         b1cost = 0;
+        // RT_B1_DEFER: the exact tests of the survivors whose pre-test passes somewhere are
+        // deferred and merged: survivors whose pass masks are disjoint share one exact-test
+        // pass, each lane testing the one sphere it passed (ksel, read per lane); a survivor
+        // whose mask meets the pending ones first runs them.  Every lane still meets its spheres
+        // in ascending index order, so (t, ind) is the sequential scan's.
+        // (Two pending spheres per lane, flushed when a lane would need a third: no better,
+        // profiles/r05z4_*.)
+        unsigned long long ru = 0;  // lanes with a pending sphere (wave-uniform)
+        int ksel = 0;               // the pending sphere of each lane in ru
+        auto flush = [&]() {
+          const float4 gs = geo[ksel];
+          sphere_candidate_if(bpos, bdir, gs, ksel, 0.0001f, t, ind, ru);
+          ru = 0;
+        };
         for (int w = 0; w < nwords; ++w) {
           // the lane index re-read here (not the kernel-wide one): otherwise the compiler keeps
           // this loop's per-lane addresses live across the whole pool and spills them to scratch
@@ -1446,7 +1466,9 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
             // copies it to a VGPR), and the broadcast read waits at once, as the loop would
             int qbase;
             asm("v_mov_b32 %0, %1" : "=v"(qbase) : "s"((int)(size_t)((const char*)qw - lbase)));
-            if (live)
+            // (RT_B1_DEFER: the loop on every lane, the live lanes picked by lm1 in the ballots, so
+            // the pending mask stays a scalar value across the loop)
+            if (RT_B1_DEFER || live)
               while (m) {
                 const int j = pop_lowest(m), k = (w << 6) + j;
                 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -1477,8 +1499,17 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
                   if (pm2 != 0) sphere_candidate_if(mk(bpos.x + z, bpos.y, bpos.z), bdir, g, k, 0.0001f, t2, i2, pm2);
                   if (i2 == 0x7fffffff) t = t2;
                 }
-                const unsigned long long pm = __builtin_amdgcn_ballot_w64(pass);
-                if (pm != 0) sphere_candidate_if(bpos, bdir, g, k, 0.0001f, t, ind, pm);
+                const unsigned long long pm = __builtin_amdgcn_ballot_w64(pass) & (RT_B1_DEFER ? lm1 : ~0ull);
+                if (RT_B1_DEFER) {
+                  if (pm != 0) {
+                    if (pm & ru) flush();
+                    ru |= pm;
+                    int kv = k;
+                    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(ksel) : "v"(ksel), "v"(kv), "s"(pm));
+                  }
+                } else if (pm != 0) {
+                  sphere_candidate_if(bpos, bdir, g, k, 0.0001f, t, ind, pm);
+                }
               }
             if (ABL == 6) lap(6);
           } else if (live) {
@@ -1489,6 +1520,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
             }
           }
         }
+        if (RT_B1_DEFER && ru != 0) flush();
         if (ABL == 7) { tsec[4] += 1; tsec[5] += (unsigned long long)__popcll(lm1); }
         if (live) {
           if (PL) plane_pass(P, bpos, bdir, 0.0001f, t, ind);
