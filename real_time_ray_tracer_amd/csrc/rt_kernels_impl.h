@@ -552,7 +552,10 @@ __device__ __forceinline__ ConeF wave_tile_cone(const FrameParams& P, int bx, in
 // by 1e-4 plus cone_misses_f's margins) are missed by every line (-1, never an occluder); the
 // rest are tested as shadow_lit does.  "Some occluder exists" does not depend on the order.
 // Must be called by every lane of the wave (ballots and shuffles).
-constexpr int kShadowConeMinObj = 8;
+#ifndef RT_SHADOW_CONE_MIN
+#define RT_SHADOW_CONE_MIN 8
+#endif
+constexpr int kShadowConeMinObj = RT_SHADOW_CONE_MIN;
 // the binary64 occluder test of shadow_ray (p_compute.glsl:155-163) for one object's float t:
 // t > 0.0001 and length(dvec3(t * l)) < len.  With |l| within 2^-18.8 of 1 (checked per ray, see
 // shadow_bounds) the binary64 length is t |l| (1 +- 2^-51), so t < len (1 - 2^-12) and
@@ -1431,6 +1434,10 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         // profiles/r05z4_*.)
         unsigned long long ru = 0;  // lanes with a pending sphere (wave-uniform)
         int ksel = 0;               // the pending sphere of each lane in ru
+        // the pre-test's direction, NaN on the lanes that are not live (their pre-test then
+        // fails, NaN >= K being false), so the ballot needs no live mask (RT_B1_DEFER)
+        f3 tdir = bdir;
+        if (RT_B1_DEFER && !live) tdir = mk(__int_as_float(0x7fc00000), __int_as_float(0x7fc00000), __int_as_float(0x7fc00000));
         auto flush = [&]() {
           const float4 gs = geo[ksel];
           sphere_candidate_if(bpos, bdir, gs, ksel, 0.0001f, t, ind, ru);
@@ -1489,7 +1496,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
                   tsec[3] += (unsigned long long)__popcll(pm);
                 }
                 // the skip as a branch on the ballot (VCC), not an exec-mask save / restore per survivor
-                const bool pass = fmaf(bdir.z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w;
+                const bool pass = fmaf(tdir.z, q.z, fmaf(tdir.y, q.y, tdir.x * q.x)) >= q.w;
                 if (ABL == 5) {  // instruction-budget ablation: each survivor iteration twice
                   float z, t2 = t;
                   int i2 = ind;
@@ -1499,7 +1506,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
                   if (pm2 != 0) sphere_candidate_if(mk(bpos.x + z, bpos.y, bpos.z), bdir, g, k, 0.0001f, t2, i2, pm2);
                   if (i2 == 0x7fffffff) t = t2;
                 }
-                const unsigned long long pm = __builtin_amdgcn_ballot_w64(pass) & (RT_B1_DEFER ? lm1 : ~0ull);
+                const unsigned long long pm = __builtin_amdgcn_ballot_w64(pass);
                 if (RT_B1_DEFER) {
                   if (pm != 0) {
                     if (pm & ru) flush();
