@@ -423,6 +423,9 @@ __device__ __forceinline__ bool bounce_cone_keep_pt(const ConeB& c, float4 g, fl
 #ifndef RT_TL_CLUSTERS
 #define RT_TL_CLUSTERS 1
 #endif
+#ifndef RT_CL_MASKS
+#define RT_CL_MASKS 1
+#endif
 #ifndef RT_GLOBAL_TAIL
 #define RT_GLOBAL_TAIL 1  // config (e), 256 spheres: 140.6 -> 128.3 ms per frame (r03i)
 #endif
@@ -439,6 +442,21 @@ __device__ __forceinline__ bool cluster_may_hit(f3 p, f3 d, float4 cb) {
   const bool line_miss = fmaf(-b, b, L2) > fmaf(Rp, Rp, 4e-6f * L2);
   const bool behind = (b + Rp) < -1e-3f * (u + Rp) && (u - Rp) > 1e-2f * (u + Rp);
   return !(line_miss || behind);
+}
+// The wave mask of the lanes (full exec mask) whose ray may hit the cluster: cluster_may_hit as
+// three ballots of single compares, !line_miss & (!c1 | !c2), each a negated compare that is true
+// on NaN (so NaN keeps the cluster, as above).  The compiler's ballot of the combined bool went
+// through a v_cndmask + v_cmp pair per cluster.
+__device__ __forceinline__ unsigned long long cluster_may_hit_mask(f3 p, f3 d, float4 cb) {
+  const float vx = cb.x - p.x, vy = cb.y - p.y, vz = cb.z - p.z;
+  const float L2 = fmaf(vz, vz, fmaf(vy, vy, vx * vx));
+  const float b = fmaf(d.z, vz, fmaf(d.y, vy, d.x * vx));
+  const float u = fast_sqrt(L2);
+  const float Rp = fmaf(0.0032f, u + 2.0f * cb.w, cb.w);
+  const unsigned long long nlm = __builtin_amdgcn_ballot_w64(!(fmaf(-b, b, L2) > fmaf(Rp, Rp, 4e-6f * L2)));
+  const unsigned long long nc1 = __builtin_amdgcn_ballot_w64(!((b + Rp) < -1e-3f * (u + Rp)));
+  const unsigned long long nc2 = __builtin_amdgcn_ballot_w64(!((u - Rp) > 1e-2f * (u + Rp)));
+  return nlm & (nc1 | nc2);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1693,11 +1711,24 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       unsigned long long kc = 0;
       for (int c = 0; c < P.ncl; c += 4) {
         const float4 c0 = clus[c], c1 = clus[c + 1], c2 = clus[c + 2], c3 = clus[c + 3];
+#if RT_CL_MASKS
+        // (the kept bits by scalar selects: the compiler's (b != 0) | ... << k went through VGPRs)
+        const unsigned long long b0 = cluster_may_hit_mask(pos, dir, c0) & hm;
+        const unsigned long long b1 = cluster_may_hit_mask(pos, dir, c1) & hm;
+        const unsigned long long b2 = cluster_may_hit_mask(pos, dir, c2) & hm;
+        const unsigned long long b3 = cluster_may_hit_mask(pos, dir, c3) & hm;
+        // (bits 4..7 first and an opaque move before the shift: with bit 0 selected directly the
+        // compiler builds it as a zero-extended bool through v_cndmask + v_readfirstlane)
+        unsigned nib = (b0 ? 16u : 0u) | (b1 ? 32u : 0u) | (b2 ? 64u : 0u) | (b3 ? 128u : 0u);
+        asm("" : "+s"(nib));
+        kc |= (unsigned long long)(nib >> 4) << c;
+#else
         const unsigned long long b0 = __builtin_amdgcn_ballot_w64(cluster_may_hit(pos, dir, c0)) & hm;
         const unsigned long long b1 = __builtin_amdgcn_ballot_w64(cluster_may_hit(pos, dir, c1)) & hm;
         const unsigned long long b2 = __builtin_amdgcn_ballot_w64(cluster_may_hit(pos, dir, c2)) & hm;
         const unsigned long long b3 = __builtin_amdgcn_ballot_w64(cluster_may_hit(pos, dir, c3)) & hm;
         kc |= (unsigned long long)((b0 != 0) | (b1 != 0) << 1 | (b2 != 0) << 2 | (b3 != 0) << 3) << c;
+#endif
       }
       // (bits of the slots past ncl need no mask: their member words are zero, rt_shim build_clusters)
       float t = -1.0f;
