@@ -8,7 +8,7 @@ L=build/v_h5/librtrt.so,real_time_ray_tracer_amd/librtrt.so
 timeout -k 10 300 python -u tools/ab.py --config d --libs $L --rounds 5 --frames 4 > $O/ab_d.txt 2>&1 &&
 timeout -k 10 300 python -u tools/ab.py --config c --libs $L --rounds 5 --frames 4 > $O/ab_c.txt 2>&1
 rc=$?
-[ $rc = 0 ] && timeout -k 10 300 python -u tools/ab.py --config e --libs $L --rounds 2 --frames 1 > $O/ab_e.txt 2>&1
+[ $rc = 0 ] && timeout -k 10 300 python -u tools/ab.py --config e --libs $L --rounds 2 --frames 2 > $O/ab_e.txt 2>&1
 python3 -c "
 import json
 for c in ('d','c'):
