@@ -1089,6 +1089,9 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
 #ifndef RT_B1_DEFER
 #define RT_B1_DEFER 1
 #endif
+#ifndef RT_B1_CREAD
+#define RT_B1_CREAD 1
+#endif
 constexpr int kAoMinWaves = RT_AO_MINW;
 template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
           int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false, bool CL = true, int DC = 0,
@@ -1498,6 +1501,11 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
             if (RT_B1_DEFER || live)
               while (m) {
                 const int j = pop_lowest(m), k = (w << 6) + j;
+#if RT_B1_CREAD
+                // the row read in C from the VGPR row base: one v_lshl_add_u32 for the address, the
+                // compiler's own wait (no inline-asm boundary, whose hazard padding cost an s_nop)
+                const float4 q = *(const float4*)(lbase + (qbase + (j << 4)));
+#else
                 typedef float v4f __attribute__((ext_vector_type(4)));
                 v4f qv;
                 int j_addr_scratch;
@@ -1505,6 +1513,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
                              : "=v"(qv), "=&v"(j_addr_scratch)
                              : "s"(j), "v"(qbase));
                 const float4 q = make_float4(qv.x, qv.y, qv.z, qv.w);  // wave-uniform address: LDS broadcast
+#endif
                 const float4 g = gw[j];
                 if (ABL == 7) {  // survivor iterations; with any pre-test pass; with any del >= 0 there
                   const bool pass = fmaf(bdir.z, q.z, fmaf(bdir.y, q.y, bdir.x * q.x)) >= q.w;
