@@ -284,16 +284,20 @@ def build_info() -> dict:
         return {"src_sha1": None, "commit": None}
 
 
-def load_traffic(cfg_name: str, src_sha1):
-    """HBM bytes per launch measured with rocprofv3 PMC passes (profiles/*_pmc.json): the newest
-    file for this config, preferring one taken on this library build (same source hash)."""
+def load_traffic(cfg_name: str, src_sha1, root: Path | None = None):
+    """HBM bytes per launch measured with rocprofv3 PMC passes (tools/pmc_summary.py): files named
+    profiles/*_pmc_<cfg>.json (as load_sq's *_sq_<cfg>.json) or the older profiles/*_pmc.json whose
+    "config" is this config; the newest by name, preferring one taken on this library build (same
+    source hash)."""
     found = []
-    for p in sorted(ROOT.glob("profiles/*_pmc.json"), reverse=True):
+    prof = (root or ROOT) / "profiles"
+    paths = set(prof.glob(f"*_pmc_{cfg_name}.json")) | set(prof.glob("*_pmc.json"))
+    for p in sorted(paths, key=lambda q: q.name, reverse=True):
         try:
             data = json.loads(p.read_text())
         except Exception:
             continue
-        if data.get("config") == cfg_name:
+        if data.get("config", cfg_name) == cfg_name:
             found.append((data, p.name))
     for data, name in found:
         if src_sha1 and data.get("src_sha1") == src_sha1:
@@ -320,8 +324,10 @@ def launch_report(args, world, rank, local_rank):
     import torch
     import torch.distributed as dist
 
-    t = torch.zeros(world, 3, dtype=torch.float64)
-    t[rank] = torch.tensor([local_rank, os.getpid(), 1.0], dtype=torch.float64)
+    # (NCCL has no CPU tensors: the report's tensor lives on the rank's GPU under nccl)
+    tdev = torch.device("cuda", local_rank) if args.backend == "nccl" and world > 1 else "cpu"
+    t = torch.zeros(world, 3, dtype=torch.float64, device=tdev)
+    t[rank] = torch.tensor([local_rank, os.getpid(), 1.0], dtype=torch.float64, device=tdev)
     if world > 1:
         dist.all_reduce(t)
     if rank == 0:
@@ -335,9 +341,10 @@ def launch_report(args, world, rank, local_rank):
         dist.destroy_process_group()
 
 
-def launch_ranks(argv) -> int:
+def launch_ranks(argv) -> int | None:
     """--gpus N > 1 without a launcher: run this script as N ranks under torch.distributed.run
-    (one process per GPU, 127.0.0.1 rendezvous on a free port) and return its exit status.  Called
+    (one process per GPU, 127.0.0.1 rendezvous on a free port) and return its exit status (None:
+    nothing launched, this process is the rank).  Called
     before anything initialises HIP in this process (nothing here touches the GPU), so the ranks
     are children of a clean parent; the parent never execs."""
     import socket
@@ -347,7 +354,7 @@ def launch_ranks(argv) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     n = ap.parse_known_args(argv)[0].gpus
     if n <= 1 or "WORLD_SIZE" in os.environ:
-        return -1
+        return None
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -385,6 +392,11 @@ def main():
                          "default) = the reference's dispatch shape, one launch and one image write per frame "
                          "(src/main.cpp:604): `value`.  >1: multi-frame launches (only the launch's last frame "
                          "writes the image) are timed instead; either way the other shape is reported beside it")
+    ap.add_argument("--link-gbps", type=float, default=0.0,
+                    help="N>1: the gather planner's per-link rate (GB/s one way into rank 0); 0 (default) = "
+                         "measured over the gather's own path before planning (dist.probe_links)")
+    ap.add_argument("--ingest-gbps", type=float, default=0.0,
+                    help="N>1 with --link-gbps: the root's ingest rate over all links (default min(N-1, 7) x link)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N>1 path with ranks sharing GPUs, gather staged through host")
     ap.add_argument("--out-stream-priority", type=int, default=0,
@@ -416,7 +428,7 @@ def main():
 
     from real_time_ray_tracer_amd import Header, Renderer, aspect_for
     from real_time_ray_tracer_amd.dist import (StripGather, StripPlan, balanced_bounds, calibrate_row_cost, equal_bounds,
-                                               imbalance)
+                                               gather_bound, gather_bounds, imbalance, probe_links)
 
     from real_time_ray_tracer_amd.dist import init_process_group
 
@@ -452,18 +464,22 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
 
-    # ---- strip plan: cost-balanced from the kernels' per-row work counters, then calibrated
-    # against each strip's measured kernel time (best of three measured plans) ------------------
+    # ---- strip plan: cost-balanced from the kernels' per-row work counters, calibrated against
+    # each strip's measured render time, and planned WITH the gather: the root strip (rank 0's,
+    # rendered in place) and the bounds minimise max(render, per-link copy, root ingest) on the
+    # link rates measured here (rt_plan_strips_gather); best of three measured plans ------------
     bounds = equal_bounds(H, world)
+    root_strip = 0
     balance_info = None
+    links = None
     if world > 1 and not args.no_balance:
         piped = mode == 1 and not args.no_pipeline
 
-        def strip_run(bnd, frames, counters):
+        def strip_run(sp, frames, counters):
             """counters: one frame's row-counter profile.  Otherwise the strip's time per frame as
             the timed run will render it: pipelined mode 1 by wall clock over 16 frames after 8,
             else the kernels' HIP-event times of the last 3 of `frames` frames."""
-            r = Renderer(W, H, S, spp, device=gpu, rows=(bnd[rank], bnd[rank + 1]))
+            r = Renderer(W, H, S, spp, device=gpu, rows=sp.rows(rank))
             r.set_stream(stream)
             if counters:
                 r.enable_counters(totals=False, rows=True)
@@ -506,31 +522,54 @@ def main():
             r.close()
             return out, ms
 
-        mine, _ = strip_run(bounds, 1, True)
+        sp0 = StripPlan(W, H, bounds)
+        mine, _ = strip_run(sp0, 1, True)
         full = torch.zeros(H, dtype=torch.float64, device=cdev)
         full[bounds[rank]:bounds[rank + 1]] = torch.from_numpy(mine).to(cdev)
         dist.all_reduce(full)
         row_cost = full.cpu().numpy()
         bounds = balanced_bounds(row_cost, world)
-        # calibration: time each strip's kernels, rescale the profile so every strip's total is
-        # its measured time, re-balance; keep the best of the measured plans (3 measurements)
+        # the link model: measured over the gather's own path (a strip's worth of bytes per
+        # transfer), unless --link-gbps states it
+        if args.link_gbps > 0:
+            links = {"link_gbps": args.link_gbps, "ingest_gbps": args.ingest_gbps if args.ingest_gbps > 0
+                     else min(world - 1, 7) * args.link_gbps, "source": "stated (--link-gbps / --ingest-gbps)"}
+        else:
+            links = probe_links(rank, world, dev, (H // world) * W * 16 if args.backend == "nccl" else 4 << 20,
+                                host_staging=args.backend == "gloo")
+            links["source"] = "measured before the plan (dist.probe_links)"
+        # calibration: time each strip's render, rescale the profile so every strip's total is its
+        # measured time (ms per row), re-plan with the gather; keep the measured plan whose bound
+        # max(measured render, link model) is smallest (3 measurements)
         measured = []
         for it in range(3):
-            _, ms = strip_run(bounds, 6 if mode in (1, 2) else 3, False)
+            sp = StripPlan(W, H, bounds, root_strip)
+            _, ms = strip_run(sp, 6 if mode in (1, 2) else 3, False)
             tt = torch.zeros(world, dtype=torch.float64, device=cdev)
-            tt[rank] = ms
+            tt[sp.strip_of(rank)] = ms
             dist.all_reduce(tt)
-            t1 = tt.cpu().tolist()
-            measured.append((max(t1), list(bounds), t1))
+            t1 = tt.cpu().tolist()  # per strip, in row order
+            per_row = np.concatenate([np.full(bounds[i + 1] - bounds[i], t1[i] / (bounds[i + 1] - bounds[i]))
+                                      for i in range(world)])
+            pred = gather_bound(per_row, bounds, root_strip, W, links["link_gbps"], links["ingest_gbps"])
+            measured.append((pred["bound_ms"], list(bounds), root_strip, t1, pred))
             if it < 2:
                 row_cost = calibrate_row_cost(bounds, row_cost, t1)
-                bounds = balanced_bounds(row_cost, world)
+                bounds, root_strip, _ = gather_bounds(row_cost, world, W, links["link_gbps"], links["ingest_gbps"])
         best = min(measured, key=lambda m: m[0])
-        bounds = best[1]
-        balance_info = {"model_bounds": measured[0][1], "model_strip_ms": [round(t, 4) for t in measured[0][2]],
-                        "model_imbalance": round(imbalance(measured[0][2]), 4),
-                        "calibrated_max_ms": [round(m[0], 4) for m in measured]}
-    plan = StripPlan(W, H, bounds)
+        bounds, root_strip = best[1], best[2]
+        balance_info = {"model_bounds": measured[0][1], "model_strip_ms": [round(t, 4) for t in measured[0][3]],
+                        "model_imbalance": round(imbalance(measured[0][3]), 4),
+                        "calibrated_max_ms": [round(max(m[3]), 4) for m in measured],
+                        "plans": [{"bounds": m[1], "root_strip": m[2], "strip_ms": [round(t, 4) for t in m[3]],
+                                   "predicted_ms": {k: round(v, 4) for k, v in m[4].items()}} for m in measured],
+                        "root_strip": root_strip,
+                        "predicted_frame_ms": {k: round(v, 4) for k, v in best[4].items()},
+                        "predicted_basis": ("max(render: each strip's measured render time, link: the largest "
+                                            "non-root strip's bytes / link_gbps, ingest: all non-root bytes / "
+                                            "ingest_gbps); rt_strip_gather_bound"),
+                        "link_model": links}
+    plan = StripPlan(W, H, bounds, root_strip)
     r0, r1 = plan.rows(rank)
     rend = Renderer(W, H, S, spp, device=gpu, rows=(r0, r1))
     if args.frame_batch > 0:
@@ -544,7 +583,8 @@ def main():
     if pipeline:
         rend.enable_pipelining(True, out_stream)
     streams = {"out": out_stream}
-    gather = StripGather(plan, rank, dev, host_staging=args.backend == "gloo") if world > 1 else None
+    gather = (StripGather(plan, rank, dev, host_staging=args.backend == "gloo", timing=args.backend == "nccl")
+              if world > 1 else None)
     state = {"frame": 0, "ref_frame": 0, "mismatch": 0, "checked": 0}
     ref = None
     # rank 0 checks gathered frames against a whole-frame render of its own: every frame with
@@ -626,6 +666,7 @@ def main():
     warm += settle
     if gather is not None:
         gather.finish()
+        gather.gather_ms(reset=True)  # the timed frames' gathers only
     torch.cuda.synchronize()
 
     # ---- timed region -----------------------------------------------------------------------
@@ -671,6 +712,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gms = gather.gather_ms(reset=True) if gather is not None and gather.timing else []
     host_wait_ms, host_waits = rend.host_stats()
     intervals = [frame_ev[i][0].elapsed_time(frame_ev[i + 1][0]) / frame_ev[i + 1][1]
                  for i in range(len(frame_ev) - 1)] if frame_ev else []
@@ -757,11 +799,17 @@ def main():
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     host_max = torch.tensor([host_s], dtype=torch.float64, device=cdev)
     strip_ms = torch.zeros(world, dtype=torch.float64, device=cdev)
-    strip_ms[rank] = sum(tot / max(n_l, 1) for n_l, tot in solo.values())  # standalone kernel ms
+    strip_ms[plan.strip_of(rank)] = sum(tot / max(n_l, 1) for n_l, tot in solo.values())  # standalone kernel ms
+    # per rank: median and mean ms from "strip rendered" to "its gather transfers complete"
+    g_ms = torch.zeros(world, 2, dtype=torch.float64, device=cdev)
+    if gms:
+        g_ms[rank, 0] = float(np.median(gms))
+        g_ms[rank, 1] = float(np.mean(gms))
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
         dist.all_reduce(host_max, op=dist.ReduceOp.MAX)
         dist.all_reduce(strip_ms)
+        dist.all_reduce(g_ms)
     elapsed = float(t_max.item())
 
     if rank == 0:
@@ -922,8 +970,25 @@ def main():
         if world > 1:
             out["collective"] = {"backend": args.backend if args.backend == "gloo" else "nccl (RCCL)",
                                  "world_size": dist.get_world_size(), "op": "batch_isend_irecv strip gather to rank 0"}
+            gm = g_ms.cpu().tolist()
             out["ranks"] = [{"rank": i, "device": devices[i]["device"], "pci_bus": devices[i]["pci_bus"],
-                             "rows": [plan.bounds[i], plan.bounds[i + 1]]} for i in range(world)]
+                             "strip": plan.strip_of(i), "rows": list(plan.rows(i)),
+                             "gather_bytes_per_frame": plan.strip_bytes(i),
+                             "gather_ms_median": round(gm[i][0], 4) if gms else None,
+                             "gather_ms_mean": round(gm[i][1], 4) if gms else None} for i in range(world)]
+            tot_b = sum(plan.strip_bytes(i) for i in range(world))
+            out["gather"] = {
+                "root_strip": plan.root_strip, "bytes_per_frame": tot_b,
+                "max_rank_bytes_per_frame": max(plan.strip_bytes(i) for i in range(world)),
+                "root_gather_ms_median": round(gm[0][0], 4) if gms else None,
+                "root_gather_ms_mean": round(gm[0][1], 4) if gms else None,
+                "measured": ("events per timed frame (nccl): on each rank's output stream before its "
+                             "batch_isend_irecv (the strip is rendered) and on a side stream ordered after the "
+                             "transfers' completion (Work.wait); rank 0's span ends when every strip has landed, "
+                             "so it includes waiting for the slowest rank's render" if gms else
+                             "not timed (gloo rehearsal: host-staged)"),
+                "link_model": links,
+                "predicted_frame_ms": balance_info["predicted_frame_ms"] if balance_info else None}
             out["launched_by"] = os.environ.get("RTRT_BENCH_LAUNCHER", "external launcher")
         if mode == 1:
             # standalone launches: in the pipelined timed region the post-process shares the GPU
@@ -964,8 +1029,8 @@ def main():
 
 if __name__ == "__main__":
     rc = launch_ranks(sys.argv[1:])
-    if rc >= 0:
-        sys.exit(rc)
+    if rc is not None:  # the launcher's status; killed by a signal (rc < 0): 128 + signal
+        sys.exit(rc if rc >= 0 else 128 - rc)
     from real_time_ray_tracer_amd.dist import run_rank
 
     run_rank(main)

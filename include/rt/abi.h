@@ -105,6 +105,12 @@ int rt_device_count(void);
 /* Wait for all of the context's work (both streams). */
 int rt_synchronize(rt_ctx* ctx);
 int rt_last_hip_error(rt_ctx* ctx);
+/* Test hook: the next query of a pinned staging buffer's "consumed" event (the uploads'
+ * ring, rt_upload_header / rt_upload_rand_buffer) reports hip_error instead of asking HIP, so a
+ * test can check that such a fault is returned (RT_E_HIP, rt_last_hip_error() == hip_error) and
+ * the buffer is not reused.  The ring's slots are queried once they have been used (after 8
+ * uploads). */
+int rt_debug_fail_next_event_query(rt_ctx* ctx, int hip_error);
 
 /* ---- device-resident path (what render() drives each frame) ------------------------ */
 /* Upload the SSBO prefix: 7 header vec4 + simple_shapes[S][5] + rand_buffer[2*spp],
@@ -230,6 +236,34 @@ int rt_group_balance(rt_group* g, const float* header, int mode, int rounds, dou
 /* Host-only strip planner (no GPU): contiguous strips of nearly equal total row_cost
  * (row_cost[y] >= 0 for y < H); bounds gets n+1 entries, each strip >= 1 row. */
 int rt_plan_strips(const double* row_cost, int H, int n, int* bounds);
+/* Host-only gather-aware planner (no GPU).  The frame the reference blits whole
+ * (src/main.cpp:783-797) is assembled on a root device that renders one strip, the root strip,
+ * into its frame rows; every other strip's image (rows * width * 16 B) crosses one link into the
+ * root each frame, overlapped with the next frame's render.  Minimises, over the bounds AND the
+ * choice of root strip, the steady-state frame bound
+ *   T = max( max_i render_i, max_{i != root} bytes_i / link_gbps, sum_{i != root} bytes_i / ingest_gbps )
+ * with render_i = sum of row_ms over strip i (ms per row, e.g. rt_calibrate_row_cost's output).
+ * link_gbps: GB/s one way over one link (<= 0: no link term); ingest_gbps: GB/s the root can take
+ * from all links at once (<= 0: no ingest term).  Of the root positions that reach the bound, the
+ * one whose strip has the most rows (fewest bytes on the links) is taken; the strips on either
+ * side of it are balanced within the bound.  bounds: n+1 entries; root_strip: the strip the root
+ * owns; bound_ms (NULL or 4 entries): T, render, link and ingest parts (rt_strip_gather_bound). */
+int rt_plan_strips_gather(const double* row_ms, int H, int n, int width, double link_gbps, double ingest_gbps,
+                          int* bounds, int* root_strip, double* bound_ms);
+/* The same bound for a given plan: bound_ms[0..3] = T, max render, max link, ingest (ms). */
+int rt_strip_gather_bound(const double* row_ms, int H, const int* bounds, int n, int root_strip, int width,
+                          double link_gbps, double ingest_gbps, double* bound_ms);
+/* Re-plan with a root strip: strip root_strip renders on devices[0] into its frame rows, strip
+ * i < root_strip on devices[i + 1], strip i > root_strip on devices[i] (contexts re-created). */
+int rt_group_set_plan(rt_group* g, const int* bounds, int root_strip);
+int rt_group_root_strip(rt_group* g);
+/* the device strip i renders on */
+int rt_group_strip_device(rt_group* g, int i);
+/* The link model rt_group_balance plans with when strips copy into the root (distinct devices or
+ * forced copies): GB/s per link and into the root.  0 (the default) = measured by the next
+ * rt_group_balance (each non-root strip's copy alone, then all at once) and kept. */
+int rt_group_set_link_model(rt_group* g, double link_gbps, double ingest_gbps);
+int rt_group_link_model(rt_group* g, double* link_gbps, double* ingest_gbps);
 /* Rescale row_cost so every strip's total equals its measured time (row shape kept). */
 int rt_calibrate_row_cost(double* row_cost, int H, const int* bounds, int n, const double* strip_ms);
 
@@ -282,7 +316,10 @@ enum {
   RT_MATH_SHADOW = 10     /* shadow_ray's occluder test (p_compute.glsl:159-161) as the
                              kernels decide it: in = (light - pos).xyz, t quads; l =
                              normalize(light - pos), len = length(light - pos); out = (l.xyz,
-                             len, 1 if t > 0.0001 && length(dvec3(t * l)) < len else 0)     */
+                             len, 1 if t > 0.0001 && length(dvec3(t * l)) < len else 0)     */,
+  RT_MATH_SIN_TABLE = 11  /* the sin's exception table (rt_sin_table.h) on this build's device code:
+                             out[2i] = 1 if entry i's binary64 sin is flagged ambiguous (so the
+                             table decides it), 0 if not, -1 past the table; out[2i+1] = its x */
 };
 int rt_selftest_math(rt_ctx* ctx, int fn, const float* in, float* out, size_t n);
 

@@ -75,6 +75,10 @@ def load():
     if hasattr(lib, "rto_sin_check_range"):  # (absent from older builds, tools/sin_change_effect.py)
         lib.rto_sin_check_range.argtypes = [C.c_uint32, C.c_int64, fp, C.POINTER(C.c_uint32), C.c_int]
         lib.rto_sin_check_range.restype = C.c_int64
+    lib.rto_set_contraction.argtypes = [C.c_int]
+    lib.rto_set_contraction.restype = None
+    lib.rto_get_contraction.argtypes = []
+    lib.rto_get_contraction.restype = C.c_int
     lib.rto_random.argtypes = [C.c_float, C.c_float]
     lib.rto_random.restype = C.c_float
     lib.rto_sphere_eval.argtypes = [fp, fp, fp, C.c_float]
@@ -116,6 +120,19 @@ def dispatch(ssbo: np.ndarray, d: rto_dims, mode: int, frame: int, image=None, n
     if rc < 0:
         raise ValueError(f"rto_dispatch rejected its arguments (mode {mode})")
     return rc
+
+
+# contraction variants of random()'s argument arithmetic (rto_set_contraction; measurement and
+# test hook: 0 = the kernels' semantics)
+C_UNFUSED_DOT, C_FUSED_SEEDS, C_FUSED_JITTER = 1, 2, 4
+
+
+def set_contraction(flags: int) -> None:
+    load().rto_set_contraction(int(flags))
+
+
+def get_contraction() -> int:
+    return int(load().rto_get_contraction())
 
 
 # ---- primitives (vectorised over numpy inputs) --------------------------------------

@@ -52,8 +52,21 @@ def det_sin(x):
         return np.sin(x.astype(np.float64)).astype(F)
 
 
+# Contraction of random()'s argument arithmetic (the GLSL leaves a*b+c to the compiler): the
+# same flags as the C oracle's rto_set_contraction.  0 = the kernels' semantics (dot() inside
+# random() fused, the seed / jitter sums as written).  C_UNFUSED_DOT = ao_compute.glsl:63-73
+# read literally (both products rounded, then the sum): this restatement's own, independent
+# form on this axis.  C_FUSED_SEEDS / C_FUSED_JITTER: the seed sums of ao_compute.glsl:152-157 /
+# 317-319 contracted as a GLSL compiler does by default.
+C_UNFUSED_DOT, C_FUSED_SEEDS, C_FUSED_JITTER = 1, 2, 4
+CONTRACTION = 0
+
+
 def grandom(sx, sy):
-    d = fma(sy, F(78.233), np.asarray(sx, F) * F(12.9898))
+    if CONTRACTION & C_UNFUSED_DOT:
+        d = (np.asarray(sx, F) * F(12.9898) + np.asarray(sy, F) * F(78.233)).astype(F)
+    else:
+        d = fma(sy, F(78.233), np.asarray(sx, F) * F(12.9898))
     m = det_sin(d) * F(43758.5453123)
     return (m - np.floor(m)).astype(F)
 
@@ -229,16 +242,25 @@ class Frame:
                 dirs = self.primary(x, y)
             else:  # ao_compute.glsl:310-323
                 s1, s2, s3, s4 = (snd[0], fst[1]), (fst[2], snd[3]), (fst[0], snd[1]), (snd[2], fst[3])
-                u = grandom(((s1[0] + px * s2[0]) - px) + s3[0], ((s1[1] + py * s2[1]) - py) + s3[1])
-                w = grandom(s4[0] * px - (s3[0] * px) * s2[0], s4[1] * py - (s3[1] * py) * s2[1])
+                if CONTRACTION & C_FUSED_JITTER:
+                    u = grandom((fma(px, s2[0], s1[0]) - px) + s3[0], (fma(py, s2[1], s1[1]) - py) + s3[1])
+                    w = grandom(fma(s4[0], px, -((s3[0] * px) * s2[0])), fma(s4[1], py, -((s3[1] * py) * s2[1])))
+                else:
+                    u = grandom(((s1[0] + px * s2[0]) - px) + s3[0], ((s1[1] + py * s2[1]) - py) + s3[1])
+                    w = grandom(s4[0] * px - (s3[0] * px) * s2[0], s4[1] * py - (s3[1] * py) * s2[1])
                 il = F(1.0) / np.sqrt(fma(w, w, u * u))
                 jx = (u * il) / F(6.0) - F(0.08333)
                 jy = (w * il) / F(6.0) - F(0.08333)
                 dirs = self.primary(x, y, jx, jy)
             # get_pt_within_unit_sphere(aa), ao_compute.glsl:143-158
-            a = grandom(fst[0] + px * snd[2], fst[1] + py * snd[3])
-            b = grandom(fst[2] - px * snd[2], fst[3] - py * snd[3])
-            e = grandom(snd[0] * px + snd[2], snd[1] * py + snd[3])
+            if CONTRACTION & C_FUSED_SEEDS:
+                a = grandom(fma(px, snd[2], fst[0]), fma(py, snd[3], fst[1]))
+                b = grandom(fma(-px, snd[2], fst[2]), fma(-py, snd[3], fst[3]))
+                e = grandom(fma(snd[0], px, snd[2]), fma(snd[1], py, snd[3]))
+            else:
+                a = grandom(fst[0] + px * snd[2], fst[1] + py * snd[3])
+                b = grandom(fst[2] - px * snd[2], fst[3] - py * snd[3])
+                e = grandom(snd[0] * px + snd[2], snd[1] * py + snd[3])
             hemi = normalize3(np.stack([a * F(2) - F(1), b * F(2) - F(1), e * F(2) - F(1)], 1))
             res = np.ones((n, 4), F)
             pos = np.broadcast_to(cam, (n, 3)).astype(F).copy()

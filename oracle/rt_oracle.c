@@ -92,9 +92,24 @@ int64_t rto_sin_check_range(uint32_t start, int64_t n, const float* got, uint32_
   return count;
 }
 
+/* Contraction of random()'s argument arithmetic (measurement hook, rto_set_contraction): the
+   GLSL leaves it to the compiler whether a*b+c is one fma or two roundings, and the hash
+   (sin * 43758.5) amplifies either choice into a different sample.  0 = this build's semantics
+   (the kernels'): dot() inside random() fused as below, the seed and jitter sums unfused, as
+   written.  RTO_C_UNFUSED_DOT: dot(st, c) = st.x*c.x + st.y*c.y with both products rounded
+   (ao_compute.glsl:63-73 read literally).  RTO_C_FUSED_SEEDS: the hemisphere seeds contracted as a
+   GLSL compiler does by default (seed1 + xy*seed4 -> fma(xy, seed4, seed1); seed2 - xy*seed4 ->
+   fma(-xy, seed4, seed2); seed3*xy + seed4 -> fma(seed3, xy, seed4); ao_compute.glsl:152-157).
+   RTO_C_FUSED_JITTER: the anti-aliasing seeds likewise (seed1 + xy*seed2 - xy + seed3 ->
+   (fma(xy, seed2, seed1) - xy) + seed3; seed4*xy - seed3*xy*seed2 -> fma(seed4, xy,
+   -((seed3*xy)*seed2)); ao_compute.glsl:317-319). */
+static int rto_contract = 0;
+void rto_set_contraction(int flags) { rto_contract = flags; }
+int rto_get_contraction(void) { return rto_contract; }
+
 /* random(vec2) — p_compute.glsl:65-75: fract(sin(dot(st, vec2(12.9898,78.233))) * 43758.5453123) */
 float rto_random(float sx, float sy) {
-  float d = fmaf(sy, 78.233f, sx * 12.9898f);
+  float d = (rto_contract & RTO_C_UNFUSED_DOT) ? sx * 12.9898f + sy * 78.233f : fmaf(sy, 78.233f, sx * 12.9898f);
   float m = rto_sin(d) * 43758.5453123f;
   return m - floorf(m);
 }
@@ -571,9 +586,16 @@ static v3 get_pt_within_unit_sphere(const octx* c, int aa, int x, int y) {
   const float* f = c->rb + (size_t)(2 * aa) * 4;
   const float* s = c->rb + (size_t)(2 * aa + 1) * 4;
   float px = (float)x, py = (float)y;
-  float a = rto_random(f[0] + px * s[2], f[1] + py * s[3]); /* seed1 + xy * seed4 */
-  float b = rto_random(f[2] - px * s[2], f[3] - py * s[3]); /* seed2 - xy * seed4 */
-  float e = rto_random(s[0] * px + s[2], s[1] * py + s[3]); /* seed3 * xy + seed4 */
+  float a, b, e;
+  if (rto_contract & RTO_C_FUSED_SEEDS) {
+    a = rto_random(fmaf(px, s[2], f[0]), fmaf(py, s[3], f[1]));
+    b = rto_random(fmaf(-px, s[2], f[2]), fmaf(-py, s[3], f[3]));
+    e = rto_random(fmaf(s[0], px, s[2]), fmaf(s[1], py, s[3]));
+  } else {
+    a = rto_random(f[0] + px * s[2], f[1] + py * s[3]); /* seed1 + xy * seed4 */
+    b = rto_random(f[2] - px * s[2], f[3] - py * s[3]); /* seed2 - xy * seed4 */
+    e = rto_random(s[0] * px + s[2], s[1] * py + s[3]); /* seed3 * xy + seed4 */
+  }
   return nrm3(mk3(a * 2.0f - 1.0f, b * 2.0f - 1.0f, e * 2.0f - 1.0f));
 }
 
@@ -674,8 +696,14 @@ static void ao_main(octx* c, int x, int y, float* image, int write_image) {
     float s2x = f[2], s2y = s[3]; /* seed2 = (rb[first].z, rb[second].w) */
     float s3x = f[0], s3y = s[1]; /* seed3 = (rb[first].x, rb[second].y) */
     float s4x = s[2], s4y = f[3]; /* seed4 = (rb[second].z, rb[first].w) */
-    float u = rto_random(((s1x + px * s2x) - px) + s3x, ((s1y + py * s2y) - py) + s3y);
-    float w = rto_random(s4x * px - (s3x * px) * s2x, s4y * py - (s3y * py) * s2y);
+    float u, w;
+    if (rto_contract & RTO_C_FUSED_JITTER) {
+      u = rto_random((fmaf(px, s2x, s1x) - px) + s3x, (fmaf(py, s2y, s1y) - py) + s3y);
+      w = rto_random(fmaf(s4x, px, -((s3x * px) * s2x)), fmaf(s4y, py, -((s3y * py) * s2y)));
+    } else {
+      u = rto_random(((s1x + px * s2x) - px) + s3x, ((s1y + py * s2y) - py) + s3y);
+      w = rto_random(s4x * px - (s3x * px) * s2x, s4y * py - (s3y * py) * s2y);
+    }
     float il = 1.0f / sqrtf(fmaf(w, w, u * u)); /* normalize(vec2) */
     float jx = (u * il) / 6.0f - 0.08333f;
     float jy = (w * il) / 6.0f - 0.08333f;

@@ -75,6 +75,10 @@ float rto_sin(float x);
  * recording the first max_bad of them in bad (the device sin's exhaustive sweep) */
 int64_t rto_sin_check_range(uint32_t start, int64_t n, const float* got, uint32_t* bad, int max_bad);
 float rto_random(float x, float y);
+/* contraction variants of random()'s argument arithmetic (measurement hook; 0 = the kernels') */
+enum { RTO_C_UNFUSED_DOT = 1, RTO_C_FUSED_SEEDS = 2, RTO_C_FUSED_JITTER = 4 };
+void rto_set_contraction(int flags);
+int rto_get_contraction(void);
 float rto_sphere_eval(const float pos[3], const float dir[3], const float center[3], float r);
 void rto_normalize3(const float v[3], float out[3]);
 /* the sphere discriminant fmaf(r, r, fmaf(b, b, -dot(pmc, pmc))) of sphere_eval_ray, and the

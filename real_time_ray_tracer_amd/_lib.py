@@ -21,7 +21,8 @@ RT_PROG_P_COMPUTE = 4
 RT_PROG_H_COMPUTE = 5
 RT_MODE_AO_PP, RT_MODE_AO, RT_MODE_PHONG, RT_MODE_PHONG_REFL = 1, 2, 3, 4
 (RT_MATH_SIN, RT_MATH_RANDOM, RT_MATH_SQRT, RT_MATH_DIV, RT_MATH_NORMALIZE, RT_MATH_SPHERE, RT_MATH_SQRT_SWEEP,
- RT_MATH_RCP_SWEEP, RT_MATH_SQRT_TAIL_SWEEP, RT_MATH_SIN_RANGE, RT_MATH_SHADOW) = range(11)
+ RT_MATH_RCP_SWEEP, RT_MATH_SQRT_TAIL_SWEEP, RT_MATH_SIN_RANGE, RT_MATH_SHADOW,
+ RT_MATH_SIN_TABLE) = range(12)
 RT_NUM_FRAMES = 8
 RT_RECURSION_DEPTH = 20
 RT_SHAPE_SPHERE, RT_SHAPE_RECTANGLE, RT_SHAPE_PLANE = 1, 3, 5
@@ -89,6 +90,16 @@ SIGNATURES = {
     "rt_plan_strips": (C.c_int, [C.POINTER(C.c_double), C.c_int, C.c_int, C.POINTER(C.c_int)]),
     "rt_calibrate_row_cost": (C.c_int, [C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_int), C.c_int,
                                         C.POINTER(C.c_double)]),
+    "rt_plan_strips_gather": (C.c_int, [C.POINTER(C.c_double), C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
+                                        C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double)]),
+    "rt_strip_gather_bound": (C.c_int, [C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int,
+                                        C.c_double, C.c_double, C.POINTER(C.c_double)]),
+    "rt_group_set_plan": (C.c_int, [_grp, C.POINTER(C.c_int), C.c_int]),
+    "rt_group_root_strip": (C.c_int, [_grp]),
+    "rt_group_strip_device": (C.c_int, [_grp, C.c_int]),
+    "rt_group_set_link_model": (C.c_int, [_grp, C.c_double, C.c_double]),
+    "rt_group_link_model": (C.c_int, [_grp, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "rt_debug_fail_next_event_query": (C.c_int, [_ctx, C.c_int]),
     "rt_enable_timing": (C.c_int, [_ctx, C.c_int]),
     "rt_kernel_stats": (C.c_int, [_ctx, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]),
     "rt_reset_stats": (C.c_int, [_ctx]),

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <cstring>
 #include <functional>
@@ -115,13 +116,24 @@ struct rt_group {
   bool have_header = false;
   Workers* workers = nullptr;
   int last_hip = 0;
-  bool force_copies = false;  // test hook: every strip but strip 0 takes the copy path
+  bool force_copies = false;  // test hook: every strip but the root strip takes the copy path
+  // the root strip: rendered on devices[0] (the frame's device) into its frame rows; strip i < root
+  // runs on devices[i + 1], strip i > root on devices[i] (root 0: strip i on devices[i])
+  int root = 0;
+  double link_gbps = 0.0, ingest_gbps = 0.0;  // the gather-aware planner's link model (0: measure)
 };
 
 namespace {
 
+// the device strip i renders on
+int strip_dev(const rt_group* g, int i) {
+  return i == g->root ? g->devices[0] : g->devices[i < g->root ? i + 1 : i];
+}
+
 // strip i renders straight into its rows of the frame (no copy)
-bool on_root(const rt_group* g, int i) { return g->devices[i] == g->devices[0] && (i == 0 || !g->force_copies); }
+bool on_root(const rt_group* g, int i) {
+  return strip_dev(g, i) == g->devices[0] && (i == g->root || !g->force_copies);
+}
 
 void destroy_strips(rt_group* g) {
   for (auto*& c : g->ctx)
@@ -148,7 +160,7 @@ int make_strips(rt_group* g) {
     rt_config c = g->cfg;
     c.row_begin = g->bounds[i];
     c.row_end = g->bounds[i + 1];
-    int rc = rt_create(g->devices[i], &c, &g->ctx[i]);
+    int rc = rt_create(strip_dev(g, i), &c, &g->ctx[i]);
     if (rc == RT_OK && g->pipelined) rc = rt_enable_pipelining(g->ctx[i], 1, nullptr);
     if (rc != RT_OK) {
       destroy_strips(g);
@@ -166,7 +178,7 @@ int copy_strip(rt_group* g, int i) {
   if (on_root(g, i)) return RT_OK;
   const int W = g->cfg.width;
   const size_t bytes = (size_t)(g->bounds[i + 1] - g->bounds[i]) * W * sizeof(float4);
-  hipError_t e = hipSetDevice(g->devices[i]);
+  hipError_t e = hipSetDevice(strip_dev(g, i));
   if (e == hipSuccess)
     e = hipMemcpyAsync(g->frame + (size_t)g->bounds[i] * W, rt_image_device_ptr(g->ctx[i]), bytes,
                        hipMemcpyDeviceToDevice, (hipStream_t)rt_image_stream(g->ctx[i]));
@@ -203,6 +215,103 @@ double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// ---- the gather-aware strip planner (rt_plan_strips_gather) ----------------------------------
+// A frame split into n contiguous row strips is assembled on a root device, which renders one
+// strip (the root strip) straight into its frame rows; every other strip's image, rows * W * 16 B,
+// crosses one link into the root once per frame, overlapped with the next frame's render.  The
+// steady-state frame time is then bounded by
+//   T = max( max_i render_i,  max_{i != root} bytes_i / link,  sum_{i != root} bytes_i / ingest ).
+// The planner minimises T over the bounds and the choice of root strip: bisection on T, each
+// candidate checked for every root position j by filling the strips below j from row 0 and
+// those above j from row H with as many rows as the render and link caps allow, then giving the
+// root the cheapest interval that covers what they leave and satisfies the ingest bound.
+struct GatherModel {
+  const double* cum;  // prefix sums of the per-row render cost (ms), H + 1 entries
+  int H, n;
+  double rl;  // ms per row over one link (0: no link term)
+  double ri;  // ms per non-root row at the root's ingest (0: no ingest term)
+};
+
+double seg_cost(const GatherModel& m, int a, int b) { return m.cum[b] - m.cum[a]; }
+
+int link_cap(const GatherModel& m, double T, int limit) {
+  if (m.rl <= 0.0) return limit;
+  const double r = std::floor(T / m.rl);
+  return r < (double)limit ? (int)r : limit;
+}
+
+// most rows (<= limit) a non-root strip starting at row y and growing up may take within T
+int rows_up(const GatherModel& m, int y, int limit, double T) {
+  const int cap = link_cap(m, T, limit);
+  if (cap <= 0) return 0;
+  const double* p = std::upper_bound(m.cum + y, m.cum + y + cap + 1, m.cum[y] + T);
+  return (int)(p - (m.cum + y)) - 1;
+}
+
+// most rows (<= limit) a non-root strip ending at row y (exclusive) and growing down may take
+int rows_down(const GatherModel& m, int y, int limit, double T) {
+  const int cap = link_cap(m, T, limit);
+  if (cap <= 0) return 0;
+  const double* p = std::lower_bound(m.cum + y - cap, m.cum + y + 1, m.cum[y] - T);
+  return y - (int)(p - m.cum);
+}
+
+// k strips covering [y0, y1) upward, each within T (rows_up caps), each >= 1 row; false if the
+// caps cannot cover the range.  b receives the k - 1 inner bounds.
+bool fill_up(const GatherModel& m, int y0, int y1, int k, double T, int* b) {
+  int y = y0;
+  for (int s = 0; s < k; ++s) {
+    const int left = k - 1 - s;  // strips after this one, one row each at least
+    int r = s == k - 1 ? y1 - y : std::min(rows_up(m, y, y1 - y - left, T), y1 - y - left);
+    if (r < 1) return false;
+    if (s == k - 1 && (seg_cost(m, y, y1) > T || (m.rl > 0.0 && r * m.rl > T))) return false;
+    y += r;
+    if (s < k - 1) b[s] = y;
+  }
+  return y == y1;
+}
+
+// the smallest per-strip bound T' <= T with which k strips still cover [y0, y1): balanced strips
+bool fill_balanced(const GatherModel& m, int y0, int y1, int k, double T, int* b) {
+  if (k == 0) return y0 == y1;
+  if (!fill_up(m, y0, y1, k, T, b)) return false;
+  double lo = 0.0, hi = T;
+  for (int it = 0; it < 60; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    std::vector<int> t(std::max(1, k - 1));
+    if (fill_up(m, y0, y1, k, mid, t.data())) hi = mid; else lo = mid;
+  }
+  return fill_up(m, y0, y1, k, hi, b);
+}
+
+// root strip j within T: the root's interval [ra, rb), or false.  Minimises the root's render cost.
+bool root_interval(const GatherModel& m, int j, double T, int& ra, int& rb) {
+  const int H = m.H, n = m.n;
+  int a = 0;  // rows [0, a) the j strips below the root can cover at most
+  for (int s = 0; s < j; ++s) {
+    const int r = rows_up(m, a, H - a - (n - 1 - s), T);
+    if (r < 1) return false;
+    a += r;
+  }
+  int b = H;  // rows [b, H) the strips above the root can cover at most
+  for (int s = n - 1; s > j; --s) {
+    const int r = rows_down(m, b, b - s, T);
+    if (r < 1) return false;
+    b -= r;
+  }
+  int need = 1;  // ingest: the non-root rows must cross into the root within T
+  if (m.ri > 0.0) need = std::max(need, H - (int)std::min((double)H, std::floor(T / m.ri)));
+  const int amax = std::min(a, H - (n - 1 - j) - 1), bmax = H - (n - 1 - j);
+  double best = -1.0;
+  for (int x = j; x <= amax; ++x) {
+    const int y = std::max(std::max(b, x + need), x + 1);
+    if (y > bmax) continue;
+    const double c = seg_cost(m, x, y);
+    if (best < 0.0 || c < best) best = c, ra = x, rb = y;
+  }
+  return best >= 0.0 && best <= T;
+}
+
 }  // namespace
 
 extern "C" {
@@ -228,6 +337,74 @@ int rt_plan_strips(const double* row_cost, int H, int n, int* bounds) {
     bounds[i] = y;
   }
   bounds[n] = H;
+  return RT_OK;
+}
+
+int rt_strip_gather_bound(const double* row_ms, int H, const int* bounds, int n, int root_strip, int width,
+                          double link_gbps, double ingest_gbps, double* bound_ms) {
+  if (!row_ms || !bounds || !bound_ms || H <= 0 || n <= 0 || width <= 0 || root_strip < 0 || root_strip >= n ||
+      !valid_bounds(bounds, n, H))
+    return RT_E_INVAL;
+  const double row_bytes = (double)width * 16.0;
+  double render = 0.0, link = 0.0, rest = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double c = 0.0;
+    for (int y = bounds[i]; y < bounds[i + 1]; ++y) c += row_ms[y];
+    render = std::max(render, c);
+    if (i == root_strip) continue;
+    const double bytes = row_bytes * (bounds[i + 1] - bounds[i]);
+    rest += bytes;
+    if (link_gbps > 0.0) link = std::max(link, bytes / (link_gbps * 1e6));
+  }
+  const double ingest = ingest_gbps > 0.0 ? rest / (ingest_gbps * 1e6) : 0.0;
+  bound_ms[0] = std::max(render, std::max(link, ingest));
+  bound_ms[1] = render;
+  bound_ms[2] = link;
+  bound_ms[3] = ingest;
+  return RT_OK;
+}
+
+int rt_plan_strips_gather(const double* row_ms, int H, int n, int width, double link_gbps, double ingest_gbps,
+                          int* bounds, int* root_strip, double* bound_ms) {
+  if (!row_ms || !bounds || !root_strip || H <= 0 || n <= 0 || n > H || width <= 0 || !(link_gbps == link_gbps) ||
+      !(ingest_gbps == ingest_gbps))
+    return RT_E_INVAL;
+  std::vector<double> cum((size_t)H + 1, 0.0);
+  for (int y = 0; y < H; ++y) {
+    if (!(row_ms[y] >= 0.0) || row_ms[y] == HUGE_VAL) return RT_E_INVAL;  // negative, NaN or inf
+    cum[y + 1] = cum[y] + row_ms[y];
+  }
+  const double row_bytes = (double)width * 16.0;
+  const GatherModel m{cum.data(), H, n, link_gbps > 0.0 ? row_bytes / (link_gbps * 1e6) : 0.0,
+                      ingest_gbps > 0.0 ? row_bytes / (ingest_gbps * 1e6) : 0.0};
+  // bisection on T: every root position is tried at every candidate
+  double lo = 0.0, hi = cum[H] + H * (m.rl + m.ri) + 1e-9;
+  auto feasible = [&](double T) {
+    int ra, rb;
+    for (int j = 0; j < n; ++j)
+      if (root_interval(m, j, T, ra, rb)) return true;
+    return false;
+  };
+  for (int it = 0; it < 100 && hi - lo > 1e-12 * std::max(1.0, hi); ++it) {
+    const double mid = 0.5 * (lo + hi);
+    if (feasible(mid)) hi = mid; else lo = mid;
+  }
+  // at the bound: of the feasible root positions the one whose strip keeps the most rows (fewest
+  // bytes on the links), its neighbours' strips balanced within the bound
+  int bj = -1, bra = 0, brb = 0;
+  for (int j = 0; j < n; ++j) {
+    int ra, rb;
+    if (root_interval(m, j, hi, ra, rb) && (bj < 0 || rb - ra > brb - bra)) bj = j, bra = ra, brb = rb;
+  }
+  if (bj < 0) return RT_E_INVAL;  // (cannot happen: hi is feasible)
+  bounds[0] = 0;
+  bounds[n] = H;
+  bounds[bj] = bra;
+  bounds[bj + 1] = brb;
+  if (!fill_balanced(m, 0, bra, bj, hi, bounds + 1) || !fill_balanced(m, brb, H, n - 1 - bj, hi, bounds + bj + 2))
+    return RT_E_INVAL;
+  *root_strip = bj;
+  if (bound_ms) return rt_strip_gather_bound(row_ms, H, bounds, n, bj, width, link_gbps, ingest_gbps, bound_ms);
   return RT_OK;
 }
 
@@ -470,9 +647,87 @@ int rt_group_download_image(rt_group* g, float* image) {
   return RT_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Links into the root device, measured: each non-root strip's image copied into its frame rows
+// alone (the per-link rate, the slowest link kept) and all at once (the root's ingest rate), by
+// wall clock over 4 copies after one.  Strips on the root device do not copy and are skipped.
+int probe_links(rt_group* g, double& link_gbps, double& ingest_gbps) {
+  std::vector<int> cp;
+  double all_bytes = 0.0;
+  for (int i = 0; i < g->n; ++i)
+    if (!on_root(g, i)) cp.push_back(i), all_bytes += (double)(g->bounds[i + 1] - g->bounds[i]) * g->cfg.width * 16.0;
+  link_gbps = ingest_gbps = 0.0;
+  if (cp.empty()) return RT_OK;
+  auto run = [&](const std::vector<int>& which, int reps) -> double {
+    for (int i : which)
+      if (rt_synchronize(g->ctx[i]) != RT_OK) return -1.0;
+    const double t0 = now_ms();
+    for (int k = 0; k < reps; ++k)
+      for (int i : which)
+        if (copy_strip(g, i) != RT_OK) return -1.0;
+    for (int i : which)
+      if (rt_synchronize(g->ctx[i]) != RT_OK) return -1.0;
+    return (now_ms() - t0) / reps;
+  };
+  double slow = -1.0;
+  for (int i : cp) {
+    if (run({i}, 1) < 0.0) return RT_E_HIP;
+    const double ms = run({i}, 4);
+    if (ms < 0.0) return RT_E_HIP;
+    const double gbps = (double)(g->bounds[i + 1] - g->bounds[i]) * g->cfg.width * 16.0 / (std::max(ms, 1e-6) * 1e6);
+    slow = slow < 0.0 ? gbps : std::min(slow, gbps);
+  }
+  if (run(cp, 1) < 0.0) return RT_E_HIP;
+  const double ms = run(cp, 4);
+  if (ms < 0.0) return RT_E_HIP;
+  link_gbps = slow;
+  ingest_gbps = all_bytes / (std::max(ms, 1e-6) * 1e6);
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_group_set_plan(rt_group* g, const int* bounds, int root_strip) {
+  if (!g || !bounds || root_strip < 0 || root_strip >= g->n || !valid_bounds(bounds, g->n, g->cfg.height))
+    return RT_E_INVAL;
+  for (auto* c : g->ctx) {
+    int rc = rt_synchronize(c);
+    if (rc != RT_OK) return rc;
+  }
+  std::copy(bounds, bounds + g->n + 1, g->bounds.begin());
+  g->root = root_strip;
+  return make_strips(g);
+}
+
+int rt_group_root_strip(rt_group* g) { return g ? g->root : RT_E_INVAL; }
+
+int rt_group_strip_device(rt_group* g, int i) {
+  if (!g || i < 0 || i >= g->n) return RT_E_INVAL;
+  return strip_dev(g, i);
+}
+
+int rt_group_set_link_model(rt_group* g, double link_gbps, double ingest_gbps) {
+  if (!g || !(link_gbps >= 0.0) || !(ingest_gbps >= 0.0)) return RT_E_INVAL;
+  g->link_gbps = link_gbps;
+  g->ingest_gbps = ingest_gbps;
+  return RT_OK;
+}
+
+int rt_group_link_model(rt_group* g, double* link_gbps, double* ingest_gbps) {
+  if (!g || !link_gbps || !ingest_gbps) return RT_E_INVAL;
+  *link_gbps = g->link_gbps;
+  *ingest_gbps = g->ingest_gbps;
+  return RT_OK;
+}
+
 int rt_group_balance(rt_group* g, const float* header, int mode, int rounds, double* strip_ms) {
   if (!g || !header || mode < RT_MODE_AO_PP || mode > RT_MODE_PHONG_REFL || rounds < 0) return RT_E_INVAL;
-  const int H = g->cfg.height, n = g->n;
+  const int H = g->cfg.height, W = g->cfg.width, n = g->n;
   const size_t nf = g->header.size();
   std::vector<float> h(header, header + nf);
   // 1. one probe frame with per-row work counters on every strip -> the frame's cost profile
@@ -493,15 +748,28 @@ int rt_group_balance(rt_group* g, const float* header, int mode, int rounds, dou
   std::vector<int> b(n + 1);
   rc = rt_plan_strips(cost.data(), H, n, b.data());
   if (rc != RT_OK) return rc;
+  int root = 0;
+  // the gather-aware plan when strips copy into the root (distinct devices, or the copy path
+  // forced): the root strip is chosen with the bounds, so the largest-byte strip stays on the root
+  // device.  The first plan is render-only (the counter profile is not in ms yet); every later one
+  // re-plans the calibrated (ms) profile with the link model, measured here unless set.
+  bool gather = g->force_copies;
+  for (int i = 1; i < n; ++i) gather = gather || g->devices[i] != g->devices[0];
   // 2. calibration: time every strip of the plan alone, as the frame loop renders it (wall
   // clock of 16 frames after 8, gather copy included), rescale the profile so each strip's
-  // total is its time, re-plan; keep the best measured plan
+  // total is its time, re-plan; keep the plan with the smallest bound (measured render, the link
+  // model's copy times)
   std::vector<int> best = b;
+  int best_root = 0;
   double best_ms = -1.0;
   std::vector<double> best_t(n, 0.0), t(n, 0.0);
   for (int it = 0; it < std::max(1, rounds); ++it) {
-    rc = rt_group_set_bounds(g, b.data());
+    rc = rt_group_set_plan(g, b.data(), root);
     if (rc != RT_OK) return rc;
+    if (gather && it == 0 && g->link_gbps <= 0.0) {
+      rc = probe_links(g, g->link_gbps, g->ingest_gbps);
+      if (rc != RT_OK) return rc;
+    }
     for (int i = 0; i < n && rc == RT_OK; ++i) {  // one strip at a time (strips may share a device)
       std::vector<float> hh(h);
       int f = strip_frames(g, i, hh.data(), mode, 0, 8, 7000, 0);
@@ -513,20 +781,33 @@ int rt_group_balance(rt_group* g, const float* header, int mode, int rounds, dou
       t[i] = (now_ms() - t0) / 16.0;
     }
     if (rc != RT_OK) return rc;
-    const double mx = *std::max_element(t.begin(), t.end());
+    double mx = *std::max_element(t.begin(), t.end());
+    if (gather) {
+      double bound[4];
+      std::vector<double> per_row(H, 0.0);  // the measured strip times spread over their rows
+      for (int i = 0; i < n; ++i)
+        for (int y = b[i]; y < b[i + 1]; ++y) per_row[y] = t[i] / (b[i + 1] - b[i]);
+      rc = rt_strip_gather_bound(per_row.data(), H, b.data(), n, root, W, g->link_gbps, g->ingest_gbps, bound);
+      if (rc != RT_OK) return rc;
+      mx = bound[0];
+    }
     if (best_ms < 0.0 || mx < best_ms) {
       best_ms = mx;
       best = b;
+      best_root = root;
       best_t = t;
     }
     if (it + 1 < rounds) {
       rc = rt_calibrate_row_cost(cost.data(), H, b.data(), n, t.data());
-      if (rc == RT_OK) rc = rt_plan_strips(cost.data(), H, n, b.data());
+      if (rc == RT_OK)
+        rc = gather ? rt_plan_strips_gather(cost.data(), H, n, W, g->link_gbps, g->ingest_gbps, b.data(), &root,
+                                            nullptr)
+                    : rt_plan_strips(cost.data(), H, n, b.data());
       if (rc != RT_OK) return rc;
     }
   }
   if (strip_ms) std::copy(best_t.begin(), best_t.end(), strip_ms);
-  return rt_group_set_bounds(g, best.data());  // fresh rings on the chosen plan
+  return rt_group_set_plan(g, best.data(), best_root);  // fresh rings on the chosen plan
 }
 
 }  // extern "C"

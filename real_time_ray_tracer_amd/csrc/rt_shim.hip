@@ -86,6 +86,7 @@ constexpr int kSchedPeriod = 16;
 
 struct rt_ctx {
   int device = 0;
+  int inject_query_error = 0;  // test hook (rt_debug_fail_next_event_query): the next staging query fails
   rt_config cfg{};
   int own0 = 0, own_rows = 0;    // strip rows
   int band0 = 0, band_rows = 0;  // strip + 1-row halo (post-process neighbours)
@@ -190,13 +191,22 @@ int staged_copy(rt_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t
   Stage& s = c->stage[c->stage_next];
   c->stage_next = (c->stage_next + 1) % kStageSlots;
   if (s.used) {
-    if (hipEventQuery(s.done) == hipErrorNotReady) {  // the GPU has not consumed it yet: wait
+    // hipErrorNotReady is "the GPU has not consumed it yet" (wait, and clear that per-thread
+    // error); any other failure is a fault of the copy or of the work before it on the stream:
+    // reported (rt_last_hip_error), never taken as "consumed" and the buffer reused
+    hipError_t q = hipEventQuery(s.done);
+    if (c->inject_query_error) {
+      q = (hipError_t)c->inject_query_error;
+      c->inject_query_error = 0;
+    }
+    if (q == hipErrorNotReady) {
+      (void)hipGetLastError();
       const auto t0 = std::chrono::steady_clock::now();
       RT_HIP(c, hipEventSynchronize(s.done));
       c->host_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       c->host_waits += 1;
-    } else {
-      (void)hipGetLastError();
+    } else if (q != hipSuccess) {
+      return hip_fail(c, q);
     }
   }
   if (s.bytes < bytes) {  // grow to a power of two >= 256 KiB: pinned allocations are slow, keep them rare
@@ -883,6 +893,12 @@ int rt_synchronize(rt_ctx* c) {
 
 int rt_last_hip_error(rt_ctx* c) { return c ? c->last_hip : 0; }
 
+int rt_debug_fail_next_event_query(rt_ctx* c, int hip_error) {
+  if (!c || hip_error == (int)hipSuccess) return RT_E_INVAL;
+  c->inject_query_error = hip_error;
+  return RT_OK;
+}
+
 }  // extern "C"
 
 namespace {
@@ -1518,12 +1534,12 @@ int rt_read_row_counters(rt_ctx* c, uint64_t* rows, int reset) {
 }
 
 int rt_selftest_math(rt_ctx* c, int fn, const float* in, float* out, size_t n) {
-  if (!c || !in || !out || fn < 0 || fn > RT_MATH_SHADOW) return RT_E_INVAL;
-  static const int in_w[] = {1, 2, 1, 2, 3, 10, 0, 0, 0, 0, 4}, out_w[] = {1, 1, 1, 1, 3, 1, 1, 1, 1, 1, 5};
+  if (!c || !in || !out || fn < 0 || fn > RT_MATH_SIN_TABLE) return RT_E_INVAL;
+  static const int in_w[] = {1, 2, 1, 2, 3, 10, 0, 0, 0, 0, 4, 0}, out_w[] = {1, 1, 1, 1, 3, 1, 1, 1, 1, 1, 5, 2};
   RT_HIP(c, hipSetDevice(c->device));
   float *din = nullptr, *dout = nullptr;
   const bool sweep = fn == RT_MATH_SQRT_SWEEP || fn == RT_MATH_RCP_SWEEP || fn == RT_MATH_SQRT_TAIL_SWEEP ||
-                     fn == RT_MATH_SIN_RANGE;  // in: one float (the count or the first bit pattern)
+                     fn == RT_MATH_SIN_RANGE || fn == RT_MATH_SIN_TABLE;  // in: one float (the count or the first bit pattern)
   size_t ib = sweep ? sizeof(float) : n * in_w[fn] * sizeof(float);
   size_t ob = n * out_w[fn] * sizeof(float);
   RT_HIP(c, hipMalloc(&din, std::max<size_t>(ib, 4)));

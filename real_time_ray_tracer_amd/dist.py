@@ -8,6 +8,12 @@ image strips into rank 0.  Strip bounds are balanced by a per-row cost profile (
 estimates from the kernels' row counters), because sky rows are far cheaper than ground rows,
 then calibrated once against each strip's measured kernel time and re-balanced.
 
+The gather is part of the plan: every non-root strip crosses one xGMI link into rank 0 each
+frame, so the planner (rt_plan_strips_gather) chooses the bounds AND which strip rank 0 owns
+(the root strip, rendered in place, never sent) to minimise max(render, per-link copy, root
+ingest).  At config (d) that puts the large, cheap sky strip on rank 0.  Rank r > 0 renders the
+r-th of the other strips in row order.
+
 The gather is pipelined: frame k's strip is gathered (async, RCCL stream) while frame k+1
 renders into the other of two image buffers.
 """
@@ -59,26 +65,67 @@ def imbalance(strip_time: list[float]) -> float:
     return float(t.max() / max(t.mean(), 1e-30) - 1.0)
 
 
+def gather_bounds(row_ms: np.ndarray, n: int, W: int, link_gbps: float, ingest_gbps: float):
+    """rt_plan_strips_gather: (bounds, root strip, predicted {bound, render, link, ingest} ms) for a
+    per-row cost profile in ms (calibrate_row_cost's output)."""
+    from .host import plan_strips_gather
+
+    return plan_strips_gather(row_ms, n, W, link_gbps, ingest_gbps)
+
+
+def gather_bound(row_ms: np.ndarray, bounds: list[int], root_strip: int, W: int, link_gbps: float,
+                 ingest_gbps: float) -> dict:
+    from .host import strip_gather_bound
+
+    return strip_gather_bound(row_ms, bounds, root_strip, W, link_gbps, ingest_gbps)
+
+
 @dataclass
 class StripPlan:
+    """Row strips [bounds[i], bounds[i+1]) and their owners: rank 0 (the gather's root) owns
+    strip root_strip, rank r > 0 the r-th of the others in row order."""
     W: int
     H: int
     bounds: list[int]
+    root_strip: int = 0
+
+    def __post_init__(self):
+        if not 0 <= self.root_strip < self.n:
+            raise ValueError(f"root strip {self.root_strip} outside 0..{self.n - 1}")
 
     @property
     def n(self) -> int:
         return len(self.bounds) - 1
 
+    def strip_of(self, rank: int) -> int:
+        """the strip index rank renders"""
+        if rank == 0:
+            return self.root_strip
+        return rank - 1 if rank - 1 < self.root_strip else rank
+
+    def rank_of(self, strip: int) -> int:
+        if strip == self.root_strip:
+            return 0
+        return strip + 1 if strip < self.root_strip else strip
+
     def rows(self, rank: int) -> tuple[int, int]:
-        return self.bounds[rank], self.bounds[rank + 1]
+        i = self.strip_of(rank)
+        return self.bounds[i], self.bounds[i + 1]
+
+    def strip_bytes(self, rank: int) -> int:
+        """bytes of rank's image strip (rgba32f rows): what it sends to rank 0 per frame (0 for rank 0)"""
+        if rank == 0:
+            return 0
+        a, b = self.rows(rank)
+        return (b - a) * self.W * 16
 
     @property
     def max_rows(self) -> int:
         return max(self.bounds[i + 1] - self.bounds[i] for i in range(self.n))
 
     def assemble(self, padded_strips: list) -> "np.ndarray | object":
-        """Concatenate the gathered (padded) strips into the [H][W][4] frame."""
-        parts = [padded_strips[i][: self.bounds[i + 1] - self.bounds[i]] for i in range(self.n)]
+        """Concatenate the gathered (padded) strips, indexed by rank, into the [H][W][4] frame."""
+        parts = [padded_strips[self.rank_of(i)][: self.bounds[i + 1] - self.bounds[i]] for i in range(self.n)]
         if isinstance(parts[0], np.ndarray):
             return np.concatenate(parts, 0)
         import torch
@@ -94,24 +141,31 @@ class StripGather:
     padding and no assembly copy (cost-balanced strips differ in height by up to ~3x, and a
     padded gather would move max_rows for every rank)."""
 
-    def __init__(self, plan: StripPlan, rank: int, device, nbuf: int = 2, root: int = 0, host_staging: bool = False):
-        """host_staging: gather through host copies (gloo rehearsal of the GPU path)."""
+    def __init__(self, plan: StripPlan, rank: int, device, nbuf: int = 2, host_staging: bool = False,
+                 timing: bool = False):
+        """host_staging: gather through host copies (gloo rehearsal of the GPU path).  timing (GPU
+        ranks): events around every gather (gather_ms)."""
         import torch
 
-        self.plan, self.rank, self.root, self.nbuf = plan, rank, root, nbuf
+        self.plan, self.rank, self.root, self.nbuf = plan, rank, 0, nbuf
         self.host_staging = host_staging
         self.device = device
         W = plan.W
         r0, r1 = plan.rows(rank)
         fdev = "cpu" if host_staging else device
         self.frames = []
-        if rank == root:
+        if rank == self.root:
             self.frames = [torch.zeros((plan.H, W, 4), dtype=torch.float32, device=fdev) for _ in range(nbuf)]
-        if rank == root and not host_staging:
+        if rank == self.root and not host_staging:
             self.strips = [f[r0:r1] for f in self.frames]  # contiguous rows of the frame
         else:
             self.strips = [torch.zeros((r1 - r0, W, 4), dtype=torch.float32, device=device) for _ in range(nbuf)]
         self.pending = [None] * nbuf
+        # timing: per gather, an event on the output stream before the sends / receives (the
+        # strip is rendered) and one on a side stream made to wait for the transfers' completion
+        self.timing = timing and not host_staging
+        self.side = torch.cuda.Stream(device) if self.timing else None
+        self.marks: list = []
 
     def strip(self, k: int):
         """Image buffer frame k renders into (waits for the gather that last used it)."""
@@ -141,7 +195,35 @@ class StripGather:
         else:
             src = self.strips[i].cpu() if self.host_staging else self.strips[i]
             ops.append(dist.P2POp(dist.isend, src, self.root))
+        e0 = None
+        if self.timing:
+            import torch
+
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         self.pending[i] = dist.batch_isend_irecv(ops) if ops else None
+        if self.timing and self.pending[i]:
+            import torch
+
+            # Work.wait() orders the current stream after the transfers (no host block): the
+            # side stream's event marks when this rank's sends / receives have completed
+            e1 = torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(self.side):
+                for w in self.pending[i]:
+                    w.wait()
+                e1.record()
+            self.marks.append((e0, e1))
+
+    def gather_ms(self, reset: bool = True) -> list[float]:
+        """ms from 'strip rendered on this rank' to 'this rank's transfers complete', per gather
+        since the last reset (synchronises).  Rank 0: until every strip has landed in its frame."""
+        import torch
+
+        torch.cuda.synchronize()
+        out = [a.elapsed_time(b) for a, b in self.marks]
+        if reset:
+            self.marks = []
+        return out
 
     def finish(self):
         for i in range(self.nbuf):
@@ -190,3 +272,58 @@ def run_rank(fn, *args, **kwargs):
         sys.stderr.flush()
         sys.stdout.flush()
         os._exit(1)
+
+
+def probe_links(rank: int, world: int, device, nbytes: int, host_staging: bool = False, reps: int = 4) -> dict:
+    """One-way transfer rates into rank 0 over the gather's own path (batch_isend_irecv: RCCL
+    send/recv over xGMI on GPUs, gloo through host with host_staging): every rank alone (the
+    slowest is the per-link rate) and all ranks at once (the root's ingest rate).  Timed on rank 0
+    by wall clock over `reps` transfers after one warm-up, each case behind a barrier; every rank
+    returns rank 0's figures."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    n_el = max(1, nbytes // 4)
+    dev = "cpu" if host_staging else device
+    bufs = [torch.empty(n_el, dtype=torch.float32, device=dev) for _ in range(world)] if rank == 0 else None
+    src = torch.ones(n_el, dtype=torch.float32, device=dev) if rank != 0 else None
+
+    def sync():
+        if not host_staging:
+            torch.cuda.synchronize()
+
+    def xfer(senders):
+        if rank == 0:
+            ops = [dist.P2POp(dist.irecv, bufs[r], r) for r in senders]
+        else:
+            ops = [dist.P2POp(dist.isend, src, 0)] if rank in senders else []
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+
+    def timed(senders):
+        xfer(senders)
+        sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            xfer(senders)
+        sync()
+        return (time.perf_counter() - t0) / reps
+
+    per = [timed([r]) for r in range(1, world)]
+    both = timed(list(range(1, world)))
+    out = torch.zeros(world + 1, dtype=torch.float64, device="cpu" if host_staging else device)
+    if rank == 0:
+        out[1:world] = torch.tensor(per, dtype=torch.float64)
+        out[world] = both
+    dist.all_reduce(out)
+    per_ms = [float(x) * 1e3 for x in out[1:world].tolist()]
+    all_ms = float(out[world].item()) * 1e3
+    rates = [nbytes / (ms * 1e6) for ms in per_ms]
+    return {"link_gbps": min(rates), "ingest_gbps": (world - 1) * nbytes / (all_ms * 1e6),
+            "per_link_gbps": [round(r, 2) for r in rates], "bytes": nbytes, "reps": reps,
+            "per_link_ms": [round(m, 4) for m in per_ms], "all_at_once_ms": round(all_ms, 4),
+            "path": "gloo through host (rehearsal)" if host_staging else "RCCL send/recv (batch_isend_irecv)"}

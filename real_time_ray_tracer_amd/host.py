@@ -323,6 +323,10 @@ class Renderer:
     def reset_stats(self):
         self._c(self._lib.rt_reset_stats(self.ctx), "rt_reset_stats")
 
+    def debug_fail_next_event_query(self, hip_error: int):
+        """Test hook (rt_debug_fail_next_event_query): the next staging-buffer query reports hip_error."""
+        self._c(self._lib.rt_debug_fail_next_event_query(self.ctx, int(hip_error)), "rt_debug_fail_next_event_query")
+
     def host_stats(self) -> tuple[float, int]:
         """(ms, count) of host waits for a free staging buffer since reset_stats (back-pressure)."""
         ms, n = C.c_double(), C.c_longlong()
@@ -346,12 +350,12 @@ class Renderer:
         return out
 
     def selftest_math(self, fn: int, inputs: np.ndarray, n: int) -> np.ndarray:
-        out_w = {_lib.RT_MATH_NORMALIZE: 3, _lib.RT_MATH_SHADOW: 5}.get(fn, 1)
+        out_w = {_lib.RT_MATH_NORMALIZE: 3, _lib.RT_MATH_SHADOW: 5, _lib.RT_MATH_SIN_TABLE: 2}.get(fn, 1)
         in_w = {_lib.RT_MATH_RANDOM: 2, _lib.RT_MATH_DIV: 2, _lib.RT_MATH_NORMALIZE: 3, _lib.RT_MATH_SPHERE: 10,
                 _lib.RT_MATH_SHADOW: 4}.get(fn, 1)
         inp = np.ascontiguousarray(inputs, np.float32).reshape(-1)
         sweep = fn in (_lib.RT_MATH_SQRT_SWEEP, _lib.RT_MATH_RCP_SWEEP, _lib.RT_MATH_SQRT_TAIL_SWEEP,
-                       _lib.RT_MATH_SIN_RANGE)
+                       _lib.RT_MATH_SIN_RANGE, _lib.RT_MATH_SIN_TABLE)
         if inp.size < (1 if sweep else n * in_w):
             raise ValueError(f"selftest_math: {inp.size} input floats for n = {n} (need {1 if sweep else n * in_w})")
         out = np.empty(n * out_w, np.float32)
@@ -413,6 +417,26 @@ class StripGroup:
         """Whether strip i's image is copied into the frame (another device, or forced)."""
         return bool(self._c(self._lib.rt_group_strip_copies(self.g, i), "rt_group_strip_copies"))
 
+    def set_plan(self, bounds, root_strip: int):
+        """rt_group_set_plan: new bounds and root strip (the strip rendered on devices[0])."""
+        b = (C.c_int * (self.n + 1))(*[int(x) for x in bounds])
+        self._c(self._lib.rt_group_set_plan(self.g, b, int(root_strip)), "rt_group_set_plan")
+
+    def root_strip(self) -> int:
+        return self._c(self._lib.rt_group_root_strip(self.g), "rt_group_root_strip")
+
+    def strip_device(self, i: int) -> int:
+        return self._c(self._lib.rt_group_strip_device(self.g, i), "rt_group_strip_device")
+
+    def set_link_model(self, link_gbps: float, ingest_gbps: float):
+        self._c(self._lib.rt_group_set_link_model(self.g, float(link_gbps), float(ingest_gbps)),
+                "rt_group_set_link_model")
+
+    def link_model(self) -> tuple[float, float]:
+        a, b = C.c_double(), C.c_double()
+        self._c(self._lib.rt_group_link_model(self.g, C.byref(a), C.byref(b)), "rt_group_link_model")
+        return a.value, b.value
+
     def force_copies(self, on: bool = True):
         """Test hook: every strip but strip 0 renders into its own image and copies it into the
         frame, as strips on other devices do (the copy path, exercised on one GPU)."""
@@ -471,6 +495,31 @@ def plan_strips(row_cost, n: int) -> list[int]:
     b = (C.c_int * (n + 1))()
     _check(_lib.load().rt_plan_strips(c.ctypes.data_as(C.POINTER(C.c_double)), c.size, n, b), "rt_plan_strips")
     return list(b)
+
+
+def plan_strips_gather(row_ms, n: int, width: int, link_gbps: float, ingest_gbps: float):
+    """rt_plan_strips_gather (host only): strips AND root strip minimising
+    max(render, per-link copy, root ingest); returns (bounds, root_strip, {T, render, link, ingest} ms)."""
+    c = np.ascontiguousarray(row_ms, np.float64)
+    b = (C.c_int * (n + 1))()
+    root = C.c_int()
+    out = (C.c_double * 4)()
+    _check(_lib.load().rt_plan_strips_gather(c.ctypes.data_as(C.POINTER(C.c_double)), c.size, n, width,
+                                             float(link_gbps), float(ingest_gbps), b, C.byref(root), out),
+           "rt_plan_strips_gather")
+    return list(b), root.value, dict(zip(("bound_ms", "render_ms", "link_ms", "ingest_ms"), list(out)))
+
+
+def strip_gather_bound(row_ms, bounds, root_strip: int, width: int, link_gbps: float, ingest_gbps: float) -> dict:
+    """rt_strip_gather_bound: the frame bound of a given plan {T, render, link, ingest} (ms)."""
+    c = np.ascontiguousarray(row_ms, np.float64)
+    n = len(bounds) - 1
+    b = (C.c_int * (n + 1))(*[int(x) for x in bounds])
+    out = (C.c_double * 4)()
+    _check(_lib.load().rt_strip_gather_bound(c.ctypes.data_as(C.POINTER(C.c_double)), c.size, b, n, int(root_strip),
+                                             width, float(link_gbps), float(ingest_gbps), out),
+           "rt_strip_gather_bound")
+    return dict(zip(("bound_ms", "render_ms", "link_ms", "ingest_ms"), list(out)))
 
 
 def calibrate_row_cost(bounds, row_cost, strip_ms) -> np.ndarray:

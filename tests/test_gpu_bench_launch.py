@@ -28,5 +28,13 @@ def test_bench_gpus_2_renders_on_2_ranks():
     assert out["n_gpus"] == 2
     assert out["verify"]["frames_checked"] >= 2 and out["verify"]["mismatched"] == 0, out["verify"]
     assert [q["rank"] for q in out["ranks"]] == [0, 1]
-    assert out["ranks"][0]["rows"][0] == 0 and out["ranks"][1]["rows"][1] == 1080
+    # the two strips partition the frame; rank 0 owns the plan's root strip (gather-aware plan,
+    # dist.probe_links measured the host-staged gloo path here) and sends nothing
+    spans = sorted(tuple(q["rows"]) for q in out["ranks"])
+    assert spans[0][0] == 0 and spans[0][1] == spans[1][0] and spans[1][1] == 1080
+    g = out["gather"]
+    assert out["ranks"][0]["strip"] == g["root_strip"] and out["ranks"][0]["gather_bytes_per_frame"] == 0
+    r1 = out["ranks"][1]["rows"]
+    assert out["ranks"][1]["gather_bytes_per_frame"] == (r1[1] - r1[0]) * 1920 * 16
+    assert g["link_model"]["link_gbps"] > 0 and g["predicted_frame_ms"]["bound_ms"] > 0
     assert out["launched_by"].startswith("bench.py --gpus 2")

@@ -56,10 +56,11 @@ def test_group_frames_equal_whole_frame(mode, spp, frames, pipelined, G):
         assert_bitwise(g.image(), want, f"G={G} mode {mode}")
 
 
-@pytest.mark.parametrize("pipelined", [False, True])
-def test_group_forced_copies_mixed_modes(pipelined):
-    """The copy path of strips on other devices (rt_group_force_copies: every strip but strip 0
-    renders into its own image and copies it into the frame), exercised on one GPU.  The copy
+@pytest.mark.parametrize("pipelined,root", [(False, 0), (True, 0), (False, 2), (True, 1)])
+def test_group_forced_copies_mixed_modes(pipelined, root):
+    """The copy path of strips on other devices (rt_group_force_copies: every strip but the root
+    strip renders into its own image and copies it into the frame), exercised on one GPU, with
+    the root on the bottom strip (0) or another one (rt_group_set_plan's owner permutation).  The copy
     runs on the stream that wrote the strip's image: the output stream after a pipelined mode-1
     frame, the main stream after modes 2-4 (which pipelined contexts still run on their main
     stream), so frames switching modes must still assemble exactly."""
@@ -73,7 +74,10 @@ def test_group_forced_copies_mixed_modes(pipelined):
         if pipelined:
             g.enable_pipelining(True)
         g.force_copies(True)
-        assert [g.strip_copies(i) for i in range(3)] == [False, True, True]
+        if root:
+            g.set_plan([0, 37, 70, 120], root)
+        assert g.root_strip() == root
+        assert [g.strip_copies(i) for i in range(3)] == [i != root for i in range(3)]
         hr, hg = h.copy(), h.copy()
         fr = fg = 0
         for k, mode in enumerate(modes):
@@ -98,6 +102,39 @@ def test_group_forced_copies_mixed_modes(pipelined):
         g.force_copies(False)
         assert not g.strip_copies(1)
     r.close()
+
+
+def test_group_balance_with_a_slow_link_gives_the_root_the_largest_strip():
+    """rt_group_balance with the copy path and a stated slow link (rt_group_set_link_model): the
+    gather-aware planner gives the root the strip with the most rows; the frames still equal the
+    whole frame bit for bit."""
+    W, H, spp = 320, 240, 4
+    h = synth(W, H, 32, spp, seed=5)
+    want, _ = whole_frames(W, H, h, 1, 10, pipelined=True)
+    with StripGroup(W, H, h.S, h.AA, devices(4)) as g:
+        g.enable_pipelining(True)
+        g.force_copies(True)
+        g.set_link_model(0.5, 1.0)
+        assert g.link_model() == (0.5, 1.0)
+        ms = g.balance(h, 1, rounds=3)
+        b = g.bounds
+        rows = [b[i + 1] - b[i] for i in range(4)]
+        root = g.root_strip()
+        assert rows[root] == max(rows), (b, root)
+        assert [g.strip_copies(i) for i in range(4)] == [i != root for i in range(4)]
+        assert len(ms) == 4 and all(t > 0 for t in ms)
+        f = g.compute_frames(h.copy(), 1, 0, 10, 7000, False)
+        assert f == 10 % 8
+        assert_bitwise(g.image(), want, f"balanced strips, root strip {root}")
+    # measured link model (no stated rates): the probe fills it in
+    with StripGroup(W, H, h.S, h.AA, devices(3)) as g:
+        g.force_copies(True)
+        g.balance(h, 2, rounds=2)
+        link, ingest = g.link_model()
+        assert link > 0 and ingest > 0
+        f = g.compute_frames(h.copy(), 2, 0, 2, 7000, False)
+        want2, _ = whole_frames(W, H, h, 2, 2)
+        assert_bitwise(g.image(), want2, "measured link model")
 
 
 def test_group_dispatch_per_frame_and_uneven_bounds():

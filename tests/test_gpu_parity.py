@@ -336,10 +336,12 @@ def _shadow_occludes_b64(l, ln, t):
 
 
 def test_shadow_occluder_decision():
-    """The kernels decide most shadow occluder tests in float (t against len (1 -+ 2^-12)) and
-    run the binary64 sequence only near len: the decision equals the binary64 one on t drawn at
-    and around both bounds, around len itself (where only the binary64 sequence decides), and
-    for degenerate light vectors (zero, tiny, huge: the float bounds are off there)."""
+    """The production kernels decide every shadow occluder test with the binary64 sequence
+    (RT_SHADOW_FAST = 0, rt_kernels_impl.h: shadow_bounds gives {0, inf}, so no decision is taken
+    in float).  Its decision equals the binary64 sequence evaluated exactly on t drawn at and
+    around len (1 -+ 2^-12) (the float fast path's bounds, kept as probe points), around len
+    itself, and for degenerate light vectors (zero, tiny, huge).  The float fast path is an A/B
+    variant only and is not compiled into librtrt.so."""
     r = Renderer(8, 8, 1, 1)
     rng = np.random.default_rng(11)
     n = 6000
@@ -419,6 +421,31 @@ def test_det_sin_exhaustive():
     r.close()
     print(f"  sin sweep: all 2^32 bit patterns, {total} mismatches, {time.time() - t0:.1f} s")
     assert total == 0, f"{total} inputs differ from the correctly rounded sin, e.g. {firsts[:8]}"
+
+
+def test_sin_table_entries_are_ambiguous_on_this_device_build():
+    """rt_sin_table.h was generated from a host build of rt_sin.h (tools/sin_enum.hip).
+    Every table entry must still be an input this build's DEVICE code flags ambiguous (else the
+    device would round its binary64 value without the table), and the device's sin must return
+    the table's correctly rounded value on each: a codegen change shows here in milliseconds,
+    beside the all-2^32 sweep above."""
+    import re
+    from pathlib import Path
+
+    txt = (Path(__file__).resolve().parents[1] / "real_time_ray_tracer_amd" / "csrc" / "rt_sin_table.h").read_text()
+    ntab = int(re.search(r"kSinTableN\s*=\s*(\d+)", txt).group(1))
+    arrays = re.findall(r"kSinTable([XY])\[\d+\]\s*=\s*\{([^}]*)\}", txt)
+    tab = {k: np.array([int(v, 16) for v in re.findall(r"0x([0-9A-Fa-f]+)u", body)], np.uint32) for k, body in arrays}
+    assert len(tab["X"]) == len(tab["Y"]) == ntab
+    r = Renderer(8, 8, 1, 1)
+    out = r.selftest_math(_lib.RT_MATH_SIN_TABLE, np.zeros(1, np.float32), ntab + 8).reshape(-1, 2)
+    vals = r.selftest_math(_lib.RT_MATH_SIN, tab["X"].view(np.float32), ntab)
+    r.close()
+    flags = out[:, 0]
+    assert np.all(flags[ntab:] == -1.0)
+    assert np.array_equal(out[:ntab, 1].view(np.uint32), tab["X"])
+    assert np.all(flags[:ntab] == 1.0), [f"0x{int(x):08x}" for x in tab["X"][flags[:ntab] != 1.0]]
+    assert np.array_equal(vals.view(np.uint32), tab["Y"])
 
 
 def test_rcp_rn_exhaustive():
