@@ -1092,14 +1092,6 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
 #ifndef RT_B1_CREAD
 #define RT_B1_CREAD 1
 #endif
-// the first bounce's pre-test two survivors at a time: the word's survivor rows compacted in
-// LDS as pairs (x0 x1 y0 y1 z0 z1 w0 w1), each pair's two dot products by packed FP32 FMAs
-// (v_pk_mul_f32 / v_pk_fma_f32: one instruction for both spheres, the same roundings as the
-// scalar dot), one skip test per pair
-#ifndef RT_B1_PAIRS
-#define RT_B1_PAIRS 0
-#endif
-typedef float rt_v2f __attribute__((ext_vector_type(2)));
 constexpr int kAoMinWaves = RT_AO_MINW;
 template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
           int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false, bool CL = true, int DC = 0,
@@ -1479,10 +1471,10 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           // this loop's per-lane addresses live across the whole pool and spills them to scratch
           const int i = (w << 6) + lane_id_here();
           bool keep;
-          float4 pt = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
           if (pt_ok) {
+            float4 pt;
             keep = i < nobj && bounce_cone_keep_pt(cb, geo[i], pt);
-            if (!RT_B1_PAIRS && i < nobj) geol[i] = pt;
+            if (i < nobj) geol[i] = pt;
           } else {
             keep = i < nobj && !bounce_cone_misses(cb, geo[i]);
           }
@@ -1493,51 +1485,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           exec_tests += (unsigned long long)__popcll(m);
           b1cost += __popcll(m);
           if (ABL == 3) tsec[6] += (unsigned long long)__popcll(m) << 24;  // sections: first-bounce survivors
-          if (RT_B1_PAIRS && pt_ok && keep) {  // survivor s's row into pair s / 2, half s & 1
-            const unsigned sr = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-            float* const pf = (float*)geol + (sr >> 1) * 8 + (sr & 1);
-            pf[0] = pt.x;
-            pf[2] = pt.y;
-            pf[4] = pt.z;
-            pf[6] = pt.w;
-          }
-          if (RT_B1_PAIRS && pt_ok) {
-            geol_valid = false;
-            __syncthreads();  // the pair rows are written
-            const float4* const gw = geo + (w << 6);
-            int qbase;  // the pair table's LDS address in a VGPR (one vector add per pair)
-            asm("v_mov_b32 %0, %1" : "=v"(qbase) : "s"((int)(size_t)((const char*)geol - lbase)));
-            // the direction, each component in both halves of a packed pair (NaN on lanes that
-            // are not live: their pre-test fails)
-            const rt_v2f dx = {tdir.x, tdir.x}, dy = {tdir.y, tdir.y}, dz = {tdir.z, tdir.z};
-            const int cnt = __popcll(m);
-            for (int sidx = 0; sidx < cnt; sidx += 2) {
-              const int j0 = pop_lowest(m);
-              const int j1 = m ? pop_lowest(m) : j0;  // (an odd count: the pair's second half is masked below)
-              const float4 A = *(const float4*)(lbase + (qbase + (sidx << 4)));       // x0 x1 y0 y1
-              const float4 B = *(const float4*)(lbase + (qbase + (sidx << 4) + 16));  // z0 z1 w0 w1
-              rt_v2f d = dx * (rt_v2f){A.x, A.y};
-              d = __builtin_elementwise_fma(dy, (rt_v2f){A.z, A.w}, d);
-              d = __builtin_elementwise_fma(dz, (rt_v2f){B.x, B.y}, d);
-              const unsigned long long pm0 = __builtin_amdgcn_ballot_w64(d.x >= B.z);
-              unsigned long long pm1 = __builtin_amdgcn_ballot_w64(d.y >= B.w);
-              if (sidx + 1 >= cnt) pm1 = 0;
-              if ((pm0 | pm1) == 0) continue;
-              if (pm0 != 0) {
-                if (pm0 & ru) flush();
-                ru |= pm0;
-                int kv = (w << 6) + j0;
-                asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(ksel) : "v"(ksel), "v"(kv), "s"(pm0));
-              }
-              if (pm1 != 0) {
-                if (pm1 & ru) flush();
-                ru |= pm1;
-                int kv = (w << 6) + j1;
-                asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(ksel) : "v"(ksel), "v"(kv), "s"(pm1));
-              }
-              (void)gw;
-            }
-          } else if (pt_ok) {
+          if (pt_ok) {
             geol_valid = false;
             __syncthreads();  // the pre-test rows are written
             if (ABL == 6) lap(5);
@@ -2332,8 +2280,7 @@ inline hipError_t launch_production(int program, const FrameParams& p, const Fra
     const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
     const long long pools = (npix + TP - 1) / TP;
     const bool tl = p.nobj <= kTailMaxObj;
-    // (tail rows rounded up to even: RT_B1_PAIRS' pair table holds ceil(survivors / 2) 32-byte pairs)
-    const size_t psh = (size_t)batch_lds(p.spp, kPool, tl ? (p.nobj + 1) & ~1 : 0).total;
+    const size_t psh = (size_t)batch_lds(p.spp, kPool, tl ? p.nobj : 0).total;
     const dim3 g((unsigned)pools), b(64);
     // timed launches pass no counters: the counter code is compiled out (fewer live scalars)
     const bool cnt = p.counters || p.row_counters;

@@ -8,8 +8,8 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method threa
 rc=$?
 echo "tests rc=$rc" >> $O/r06a_tests.txt
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 240 python -u tools/ab.py --config d --libs real_time_ray_tracer_amd/librtrt.so,build/v_pairs/librtrt.so \
+timeout -k 10 240 python -u tools/ab.py --config d --libs real_time_ray_tracer_amd/librtrt.so,build/v_pairs/librtrt.so,build/v_quads/librtrt.so \
   --rounds 4 --frames 4 > $O/r06a_ab_pairs_d.txt 2>&1 || exit $?
-timeout -k 10 240 python -u tools/ab.py --config c --libs real_time_ray_tracer_amd/librtrt.so,build/v_pairs/librtrt.so \
+timeout -k 10 240 python -u tools/ab.py --config c --libs real_time_ray_tracer_amd/librtrt.so,build/v_pairs/librtrt.so,build/v_quads/librtrt.so \
   --rounds 4 --frames 4 > $O/r06a_ab_pairs_c.txt 2>&1 || exit $?
 exit $rc

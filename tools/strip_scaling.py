@@ -1,10 +1,16 @@
 #!/usr/bin/env python
 """Single-GPU estimate of strong-scaling efficiency before the driver's multi-GPU run: time
 each rank's strip of an N-way split on its own (pipelined mode 1, as bench.py runs it) and
-compare the slowest strip with the whole frame / N.  The gather is not included.
+compare the slowest strip with the whole frame / N.  With --calibrate the plans after the
+first are gather-aware (rt_plan_strips_gather, as bench.py plans them): the root strip (rank 0's,
+never sent) and the bounds minimise max(render, per-link copy, root ingest) at a STATED link rate
+(--link-gbps, default 76.8 GB/s = one direction of one 153.6 GB/s xGMI link, MI355X), and the
+estimate is reported with and without that link bound (the copies themselves cannot run on a
+one-GPU box).
 
-    python tools/strip_scaling.py --config d --n 8 --frames 20
+    python tools/strip_scaling.py --config d --n 8 --frames 20 --calibrate --warm-ms 300
 """
+import json
 import argparse
 import sys
 import time
@@ -17,7 +23,8 @@ sys.path.insert(0, str(ROOT))
 
 from bench import CONFIGS, config_header  # noqa: E402
 from real_time_ray_tracer_amd import Header, Renderer, aspect_for  # noqa: E402
-from real_time_ray_tracer_amd.dist import balanced_bounds, equal_bounds  # noqa: E402
+from real_time_ray_tracer_amd.dist import (balanced_bounds, equal_bounds, gather_bound,  # noqa: E402
+                                           gather_bounds)
 
 
 def frame_ms(W, H, S, spp, mode, h, rows, frames, warm=8, kernels=False, multi=False):
@@ -88,8 +95,16 @@ def main():
     ap.add_argument("--calibrate", action="store_true",
                     help="bench.py's calibration: time the plan's strips (pipelined frames for mode 1), rescale the profile, "
                          "re-balance; best of three measured plans")
+    ap.add_argument("--link-gbps", type=float, default=76.8,
+                    help="stated one-way rate of one xGMI link into the root (GB/s) for the gather-aware plans")
+    ap.add_argument("--ingest-gbps", type=float, default=0.0, help="root ingest rate (default min(n-1, 7) x link)")
+    ap.add_argument("--save-profile", default="", help="write the calibrated per-row ms profile and plan (JSON)")
     a = ap.parse_args()
     W, H, S, spp, mode, _ = CONFIGS[a.config]
+    link = a.link_gbps
+    ingest = a.ingest_gbps or min(a.n - 1, 7) * link
+    root = 0
+    row_ms = None
     mode = a.mode or mode
     frame_ms.warm_ms = a.warm_ms
     h = config_header(a.config)
@@ -111,12 +126,15 @@ def main():
             measured = []
             for it in range(3):
                 t = [frame_ms(W, H, S, spp, mode, h, (b[i], b[i + 1]), 16, warm=8, kernels=mode != 1) for i in range(a.n)]
-                measured.append((max(t), list(b)))
-                print(f"calibration plan {it}: {b} strip ms {[round(x, 3) for x in t]}")
+                per_row = np.concatenate([np.full(b[i + 1] - b[i], t[i] / (b[i + 1] - b[i])) for i in range(a.n)])
+                pred = gather_bound(per_row, b, root, W, link, ingest)
+                measured.append((pred["bound_ms"], list(b), root, t, per_row))
+                print(f"calibration plan {it}: {b} root strip {root} strip ms {[round(x, 3) for x in t]} predicted "
+                      f"{ {k: round(v, 4) for k, v in pred.items()} }")
                 if it < 2:
                     cost = calibrate_row_cost(b, cost, t)
-                    b = balanced_bounds(cost, a.n)
-            b = min(measured, key=lambda m: m[0])[1]
+                    b, root, _ = gather_bounds(cost, a.n, W, link, ingest)
+            _, b, root, _, row_ms = min(measured, key=lambda m: m[0])
     strips, host = [], []
     for i in range(a.n):
         if a.only >= 0 and i != a.only:
@@ -131,6 +149,18 @@ def main():
     print(f"ideal {full / a.n:.3f} ms, slowest strip {max(strips):.3f} ms -> efficiency "
           f"{full / a.n / max(strips):.3f} (balance {np.mean(strips) / max(strips):.3f}, "
           f"sum of strips / whole {sum(strips) / full:.3f})")
+    per_row = np.concatenate([np.full(b[i + 1] - b[i], strips[i] / (b[i + 1] - b[i])) for i in range(a.n)])
+    g = gather_bound(per_row, b, root, W, link, ingest)
+    sent = [(b[i + 1] - b[i]) * W * 16 for i in range(a.n) if i != root]
+    print(f"gather (stated link {link} GB/s, ingest {ingest} GB/s): root strip {root} ({b[root + 1] - b[root]} rows), "
+          f"largest sent strip {max(sent) / 1e6 if sent else 0:.1f} MB, link bound {g['link_ms']:.3f} ms, ingest bound "
+          f"{g['ingest_ms']:.3f} ms -> frame bound {g['bound_ms']:.3f} ms, efficiency with the gather "
+          f"{full / a.n / g['bound_ms']:.3f}")
+    if a.save_profile:
+        Path(a.save_profile).write_text(json.dumps({
+            "config": a.config, "n": a.n, "bounds": b, "root_strip": root, "strip_ms": strips, "whole_frame_ms": full,
+            "link_gbps": link, "ingest_gbps": ingest, "predicted": g,
+            "row_ms_calibrated": [round(float(x), 9) for x in (row_ms if row_ms is not None else per_row)]}) + "\n")
 
 
 if __name__ == "__main__":
