@@ -1330,6 +1330,16 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           nn = normalize(curr - xyz(gc));
         }
         if (aa == 0 && first) prec[lp] = make_float4(nn.x, nn.y, nn.z, t);
+        if (ABL == 9) {  // instruction-budget ablation: the hit shading's arithmetic twice
+          float z;
+          asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+          const f3 c2 = cam + (t + z) * dr;
+          const f3 n2 = normalize(c2 - (PL ? xyz(P.shapes[ind]) : xyz(gc)));
+          const float d2 = dot(dr, n2);
+          const f3 R2 = normalize(mk(dr.x - 2.0f * (d2 * n2.x), dr.y - 2.0f * (d2 * n2.y), dr.z - 2.0f * (d2 * n2.z)));
+          const f3 X2 = normalize(ax.y > 0.999f ? hm + n2 : R2 + ax.y * hm);
+          if (__float_as_uint(X2.x + X2.y + X2.z) == 0x7fc00001u) t = X2.x;
+        }
         ps = curr;
         const float reflect = ax.y;
         f3 X;
@@ -1383,6 +1393,16 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         vp = div_rn_by(py + jy, P.fH, P.inv_H);
       }
       bdir = primary_dir(P, hp, vp);
+      if (ABL == 10) {  // instruction-budget ablation: the primary setup after the hashes twice
+        float z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        float u2 = hp + z, w2 = vp + z;
+        normalize2(u2, w2);
+        const float jx2 = aa == 0 ? 0.0f : div_rn_by(u2, 6.0f, kInv6) - 0.08333f;
+        const float jy2 = aa == 0 ? 0.0f : div_rn_by(w2, 6.0f, kInv6) - 0.08333f;
+        const f3 d2 = primary_dir(P, div_rn_by(px + jx2, P.fW, P.inv_W), div_rn_by(py + jy2, P.fH, P.inv_H));
+        if (__float_as_uint(d2.x + d2.y + d2.z) == 0x7fc00001u) bdir.x = d2.y;
+      }
       // get_pt_within_unit_sphere(aa), hoisted: it depends on aa and the pixel only, so it is
       // computed once per sample — after the primary hit when LAZY, for hits only (a non-emissive
       // hit uses it)
@@ -1448,6 +1468,19 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         float t = -1.0f;
         int ind = -1;
         b1cost = 0;
+        if (ABL == 12) {  // instruction-budget ablation: the first bounce's cone and cull twice
+          float z;
+          asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+          const ConeB c2 = bounce_cone(live, mk(bpos.x + z, bpos.y, bpos.z), bdir, lm1);
+          unsigned long long acc = 0;
+          for (int w = 0; w < nwords; ++w) {
+            const int i = (w << 6) + lane_id_here();
+            float4 pt;
+            const bool k2 = i < nobj && bounce_cone_keep_pt(c2, geo[i], pt);
+            acc ^= __ballot(k2 && pt.w != 7.0f);
+          }
+          if (acc == 0x123456789abcdefull) b1cost = 1;
+        }
         // RT_B1_DEFER: the exact tests of the survivors whose pre-test passes somewhere are
         // deferred and merged: survivors whose pass masks are disjoint share one exact-test
         // pass, each lane testing the one sphere it passed (ksel, read per lane); a survivor
@@ -1598,6 +1631,15 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       float hx = __shfl(bhemi.x, src), hy = __shfl(bhemi.y, src), hz = __shfl(bhemi.z, src);
       float cr = __shfl(br, src), cg = __shfl(bg, src), cb = __shfl(bb, src);
       int ci = __shfl(bitem, src);
+      if (ABL == 11) {  // instruction-budget ablation: the hand-out's 13 shuffles twice
+        int zi;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(zi));
+        const int s2 = src + zi;
+        float q = __shfl(bpos.x, s2) + __shfl(bpos.y, s2) + __shfl(bpos.z, s2) + __shfl(bdir.x, s2) + __shfl(bdir.y, s2) +
+                  __shfl(bdir.z, s2) + __shfl(bhemi.x, s2) + __shfl(bhemi.y, s2) + __shfl(bhemi.z, s2) + __shfl(br, s2) +
+                  __shfl(bg, s2) + __shfl(bb, s2) + (float)__shfl(bitem, s2);
+        if (__float_as_uint(q) == 0x7fc00001u) cr = q;
+      }
       if (get) {
         pos = mk(sx, sy, sz);
         dir = mk(dx, dy, dz);
@@ -1744,6 +1786,22 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       // (bits of the slots past ncl need no mask: their member words are zero, rt_shim build_clusters)
       float t = -1.0f;
       int ind = -1;
+      if (ABL == 13) {  // instruction-budget ablation: the cluster cull twice
+        float z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        const f3 p2 = mk(pos.x + z, pos.y, pos.z);
+        unsigned long long k2 = 0;
+        for (int c = 0; c < P.ncl; c += 4) {
+          const unsigned long long b0 = cluster_may_hit_mask(p2, dir, clus[c]) & hm;
+          const unsigned long long b1 = cluster_may_hit_mask(p2, dir, clus[c + 1]) & hm;
+          const unsigned long long b2 = cluster_may_hit_mask(p2, dir, clus[c + 2]) & hm;
+          const unsigned long long b3 = cluster_may_hit_mask(p2, dir, clus[c + 3]) & hm;
+          unsigned nib = (b0 ? 16u : 0u) | (b1 ? 32u : 0u) | (b2 ? 64u : 0u) | (b3 ? 128u : 0u);
+          asm("" : "+s"(nib));
+          k2 |= (unsigned long long)(nib >> 4) << c;
+        }
+        if (k2 == 0x123456789abcdefull) t = 1.0f;
+      }
       for (int w = 0; w < nwords; ++w) {
         unsigned long long m = clm[w];
         // the kept clusters' member words, up to four requested per round trip (a repeated index

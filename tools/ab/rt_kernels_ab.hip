@@ -193,7 +193,7 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 0, true>), g, b, psh, stream, q, q.sph);
   else if (variant == 11)
     hipLaunchKernelGGL((ao_batch_kernel<7, false>), g, b, psh, stream, q, q.sph);
-  else if (variant >= 101 && variant <= 105 && tl && p.spp == 16 && p.nplanes == 0 && q.ncl > 0) {
+  else if (variant >= 101 && variant <= 110 && tl && p.spp == 16 && p.nplanes == 0 && q.ncl > 0) {
     // instruction budget (tools/sq_budget.sh): the production (d) instantiation (no counters,
     // depth 20, clusters) and its ablations, each repeating one section's work once more:
     // 101 none, 102 cluster-round tests (ABL 1), 103 culled primary tests (ABL 2), 104 the five
@@ -204,6 +204,14 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
     if (variant == 103) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 2, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
     if (variant == 104) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 4, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
     if (variant == 105) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 5, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
+    // round 6: 106 the hit shading's arithmetic (ABL 9), 107 the primary setup after the hashes
+    // (ABL 10), 108 the hand-out shuffles (ABL 11), 109 the first bounce's cone + cull (ABL 12),
+    // 110 the full rounds' cluster cull (ABL 13)
+    if (variant == 106) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 9, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
+    if (variant == 107) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 10, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
+    if (variant == 108) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 11, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
+    if (variant == 109) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 12, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
+    if (variant == 110) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 13, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
   } else if (variant == 91)
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 1>), g, b, psh, stream, q, q.sph);
   else if (variant == 92)
