@@ -378,6 +378,26 @@ __device__ __forceinline__ void sphere_candidate(f3 pos, f3 dir, float4 g, int i
   }
 }
 
+// sphere_candidate for a ray from the camera, with the sphere's camera-relative row q = (pmc, pp)
+// precomputed: pmc = cam - centre and pp = dot(pmc, pmc), the values sphere_candidate computes
+// first (rt_shim pack_header, the same binary32 operations), and the radius r.  Bit for bit the
+// same (t, ind) as sphere_candidate(cam, dir, g, ...).
+__device__ __forceinline__ void sphere_candidate_rel(f3 dir, float4 q, float r, int i, float thr, float& t, int& ind) {
+  const float b = dot(dir, xyz(q));
+  const float del = fmaf(r, r, fmaf(b, b, -q.w));
+  const bool hit = del >= 0.0f;
+  if (__builtin_amdgcn_ballot_w64(hit) != 0) {
+    // the tail of sphere_candidate (see there)
+    float s = thr >= 1e-6f ? sqrt_rn_tail(del) : sqrt_rn(del);
+    float t1 = -1.0f * b + s;
+    float t2 = -1.0f * b - s;
+    float res = __uint_as_float(min(__float_as_uint(t1), __float_as_uint(t2)));
+    const bool acc = hit & (res > thr) & (__float_as_uint(res) < __float_as_uint(t));
+    t = acc ? res : t;
+    ind = acc ? i : ind;
+  }
+}
+
 // sphere_candidate for the lanes with `on` only (the others run the arithmetic and accept nothing):
 // callers branch on a wave-uniform ballot of `on` instead of masking exec per lane.
 __device__ __forceinline__ void sphere_candidate_if(f3 pos, f3 dir, float4 g, int i, float thr, float& t, int& ind,

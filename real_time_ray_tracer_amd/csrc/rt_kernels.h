@@ -55,6 +55,7 @@ struct FrameParams {
   // AO bounce-ray cluster culling (set by the host, rt_shim build_clusters; ncl = 0: off):
   const float4* clus;        // [ncl] (centre, R): every member sphere lies within R of the centre
   const unsigned long long* clmask;  // [1 + kMaxClusters][kClusterWords]: always-tested spheres, then members
+  const float4* camrel;              // [S] (camera - centre, |camera - centre|^2 as the kernels' dot) per sphere
   int ncl;
   const float4* rb;          // rand_buffer[2*spp]
   float4* out_pix;           // colour destination [band_rows][W]
@@ -101,14 +102,18 @@ constexpr int kClusterWords = 4;
 //   [5S, 7S)         planes: 2 float4 per plane, compacted, ascending index
 //   [7S, 7S + 64)    clusters: (centre, R) per cluster
 //   then (1 + 64) * 4 u64 cluster masks (the always-tested spheres, then each cluster's members)
+//   then [S) camrel: per sphere (camera - centre, dot of it with itself), NaN for other shapes:
+//        the camera rays' sphere tests without the per-lane subtraction and self dot (phong /
+//        hybrid primary rays; the same float operations, done once per frame on the host)
 //   then rand_buffer[2 spp]
 __host__ __device__ constexpr size_t sphere_table(int S) { return (size_t)4 * S; }
 __host__ __device__ constexpr size_t plane_table(int S) { return (size_t)5 * S; }
 __host__ __device__ constexpr size_t cluster_table(int S) { return (size_t)7 * S; }
 __host__ __device__ constexpr size_t cluster_mask_table(int S) { return cluster_table(S) + kMaxClusters; }
-__host__ __device__ constexpr size_t rand_table(int S) {
+__host__ __device__ constexpr size_t camrel_table(int S) {
   return cluster_mask_table(S) + (size_t)(1 + kMaxClusters) * kClusterWords / 2;
 }
+__host__ __device__ constexpr size_t rand_table(int S) { return camrel_table(S) + (size_t)S; }
 __host__ __device__ constexpr size_t table_vec4(int S, int spp) { return rand_table(S) + (size_t)2 * spp; }
 
 enum KernelId { K_AOP = 1, K_POST = 2, K_AO = 3, K_PHONG = 4, K_HYBRID = 5 };

@@ -534,12 +534,17 @@ __device__ __forceinline__ int closest_hit_cone(const FrameParams& P, const floa
   float t = -1.0f;
   int ind = -1;
   const int lane = threadIdx.x & 63;
+  // cam is the header's camera (P.cx, P.cy, P.cz): the survivors are tested from the per-frame
+  // camera-relative rows (P.camrel: cam - centre and its self dot, computed on the host with the
+  // same float operations), so each test skips the three subtractions and the self dot
+  const float4* const cr = P.camrel;
   auto word = [&](int w, bool keep) {
     unsigned long long m = uniform_mask(__ballot(keep));
     const float4* const gw = geo + w;  // (unsigned row offset: one scalar shift per survivor)
+    const float4* const cw = cr + w;
     while (m && !SKIP) {
       const unsigned j = (unsigned)pop_lowest(m);
-      sphere_candidate(cam, dir, gw[j], w + (int)j, thr, t, ind);
+      sphere_candidate_rel(dir, cw[j], gw[j].w, w + (int)j, thr, t, ind);
     }
   };
   int w = 0;
@@ -1092,6 +1097,11 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
 #ifndef RT_B1_CREAD
 #define RT_B1_CREAD 1
 #endif
+// the primary rays' culled sphere tests from the camera-relative rows (P.camrel, as the Phong /
+// hybrid camera rays); 0 = from the sphere rows (the camera in VGPRs)
+#ifndef RT_AO_CAMREL
+#define RT_AO_CAMREL 0
+#endif
 constexpr int kAoMinWaves = RT_AO_MINW;
 template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
           int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false, bool CL = true, int DC = 0,
@@ -1438,7 +1448,8 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         while (m) {
           const unsigned j = (unsigned)pop_lowest(m);
           const int i = (w << 6) + (int)j;
-          sphere_candidate(bpos, bdir, gw[j], i, 0.0001f, t, ind);
+          if (RT_AO_CAMREL) sphere_candidate_rel(bdir, P.camrel[i], gw[j].w, i, 0.0001f, t, ind);
+          else sphere_candidate(bpos, bdir, gw[j], i, 0.0001f, t, ind);
           if (ABL == 2) {  // timing ablation: the culled primary tests twice
             float z;
             asm volatile("v_mov_b32 %0, 0" : "=v"(z));
@@ -2305,6 +2316,7 @@ inline FrameParams launch_params(const FrameParams& p) {
   q.planes = p.shapes + plane_table(p.S);
   q.clus = p.shapes + cluster_table(p.S);
   q.clmask = (const unsigned long long*)(p.shapes + cluster_mask_table(p.S));
+  q.camrel = p.shapes + camrel_table(p.S);
   q.b1_min = 1;
   {  // rotation group: the pools of one image row (at least 8)
     const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;

@@ -1022,6 +1022,16 @@ int pack_header(rt_ctx* c, const float* h, float4* tab, int& nobj, int& nplanes,
     tab[(size_t)2 * Sc - 1] = make_float4(bg[0], bg[1], bg[2], bg[3]);
   }
   std::memcpy(tab + rt::rand_table(Sc), h + rt_off_rand(S) / 4, (size_t)2 * spp * sizeof(float4));
+  {  // camera-relative sphere rows: pmc = camera - centre, pp = dot(pmc, pmc) as the kernels'
+    // sphere_candidate forms them (binary32, fmaf; this file is built with -ffp-contract=off)
+    const float* cam = h + RT_HDR_CAMERA_LOCATION * 4;
+    float4* crel = tab + rt::camrel_table(Sc);
+    for (int i = 0; i < Sc; ++i) {
+      const float4 g = sph[i];
+      const float px = cam[0] - g.x, py = cam[1] - g.y, pz = cam[2] - g.z;
+      crel[i] = make_float4(px, py, pz, std::fmaf(pz, pz, std::fmaf(py, py, px * px)));
+    }
+  }
   nplanes = np;
   ncl = build_clusters(sph, nobj, tab + rt::cluster_table(Sc), (unsigned long long*)(tab + rt::cluster_mask_table(Sc)));
   return RT_OK;
