@@ -1097,11 +1097,6 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
 #ifndef RT_B1_CREAD
 #define RT_B1_CREAD 1
 #endif
-// the primary rays' culled sphere tests from the camera-relative rows (P.camrel, as the Phong /
-// hybrid camera rays); 0 = from the sphere rows (the camera in VGPRs)
-#ifndef RT_AO_CAMREL
-#define RT_AO_CAMREL 0
-#endif
 constexpr int kAoMinWaves = RT_AO_MINW;
 template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
           int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false, bool CL = true, int DC = 0,
@@ -1448,8 +1443,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
         while (m) {
           const unsigned j = (unsigned)pop_lowest(m);
           const int i = (w << 6) + (int)j;
-          if (RT_AO_CAMREL) sphere_candidate_rel(bdir, P.camrel[i], gw[j].w, i, 0.0001f, t, ind);
-          else sphere_candidate(bpos, bdir, gw[j], i, 0.0001f, t, ind);
+          sphere_candidate(bpos, bdir, gw[j], i, 0.0001f, t, ind);
           if (ABL == 2) {  // timing ablation: the culled primary tests twice
             float z;
             asm volatile("v_mov_b32 %0, 0" : "=v"(z));
