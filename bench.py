@@ -585,7 +585,7 @@ def main():
     streams = {"out": out_stream}
     gather = (StripGather(plan, rank, dev, host_staging=args.backend == "gloo", timing=args.backend == "nccl")
               if world > 1 else None)
-    state = {"frame": 0, "ref_frame": 0, "mismatch": 0, "checked": 0}
+    state = {"frame": 0, "ref_frame": 0, "mismatch": 0, "checked": 0, "verify_on": True, "phase": "warm-up"}
     ref = None
     # rank 0 checks gathered frames against a whole-frame render of its own: every frame with
     # --verify, otherwise (N > 1) the first VERIFY_FIRST frames, during the warm-up, so every
@@ -611,8 +611,8 @@ def main():
         if bad.any():
             state["mismatch"] += 1
             ys = np.nonzero(bad.any(axis=1))[0]
-            state.setdefault("diag", []).append({"frame": k, "pixels": int(bad.sum()), "rows": [int(ys.min()), int(ys.max())],
-                                                 "nrows": int(len(ys))})
+            state.setdefault("diag", []).append({"frame": k, "phase": state["phase"], "pixels": int(bad.sum()),
+                                                 "rows": [int(ys.min()), int(ys.max())], "nrows": int(len(ys))})
         _t.cuda.synchronize()
 
     def step(k: int):
@@ -630,7 +630,7 @@ def main():
         if gather is not None:
             with torch.cuda.stream(streams["out"]):
                 gather.gather(k)
-        if ref is not None and (args.verify or k < VERIFY_FIRST):
+        if ref is not None and state["verify_on"] and (args.verify or k < VERIFY_FIRST):
             verify(k)
 
     # One GPU, sequential modes: the frame loop runs in C++ (rt_compute_frames, the render loop of
@@ -670,6 +670,7 @@ def main():
     torch.cuda.synchronize()
 
     # ---- timed region -----------------------------------------------------------------------
+    state["phase"] = "timed"
     # per-launch HIP events only where the timed launches are the kernel durations (sequential);
     # pipelined, the roofline uses the standalone launches below and the events are host cost
     rend.enable_timing(not pipeline and not host_loop)
@@ -749,6 +750,7 @@ def main():
     # un-timed) on the timed frames' inputs -------------------------------------------------
     if gather is not None:
         gather.finish()
+    state["phase"] = "standalone"
     if pipeline:
         rend.enable_pipelining(False)
         streams["out"] = stream
@@ -770,6 +772,10 @@ def main():
     # the last rendered slot re-rendered with its own header (a trace pass rewrites identical
     # values; a post-process re-filters its previous output: the same flag-, history- and
     # byte-pattern, since those follow the normals and depth)
+    # the bursts below re-run the last slot's programs in place (a post-process re-filters its own
+    # output), so the ring no longer holds the frames the whole-frame reference renders: the
+    # gathered frames are checked up to here (warm-up, timed and standalone frames), not after
+    state["verify_on"] = False
     burst = {}
     if True:
         slot = (state["frame"] - 1) % rend.F
@@ -964,7 +970,8 @@ def main():
             out["config"]["balance"] = balance_info
         if ref is not None:
             out["verify"] = {"frames_checked": state["checked"], "mismatched": state["mismatch"],
-                             "what": ("every frame" if args.verify else f"the first {VERIFY_FIRST} frames (warm-up)")
+                             "what": ("every frame up to the kernel-time bursts (warm-up, settle, timed and standalone "
+                                      "frames)" if args.verify else f"the first {VERIFY_FIRST} frames (warm-up)")
                              + ": the gathered frame vs a whole-frame render on rank 0, bit for bit",
                              "diag": state.get("diag", [])[:6]}
         if world > 1:
