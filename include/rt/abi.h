@@ -199,8 +199,9 @@ int rt_group_create(int n, const int* devices, const rt_config* cfg, const int* 
 /* Strip i's copy path: 1 = its image is copied into the frame (another device, peer access
  * on, or forced below), 0 = it renders straight into its frame rows; < 0 on a bad argument. */
 int rt_group_strip_copies(rt_group* g, int i);
-/* Test hook: on != 0 makes every strip but strip 0 render into its own image and copy it into
- * the frame, even on the root device (the copy path of distinct devices, on one GPU). */
+/* Test hook: on != 0 makes every strip but the root strip (rt_group_root_strip; strip 0 unless a
+ * plan moved it) render into its own image and copy it into the frame, even on the root device
+ * (the copy path of distinct devices, on one GPU). */
 int rt_group_force_copies(rt_group* g, int on);
 int rt_group_destroy(rt_group* g);
 int rt_group_size(rt_group* g);
@@ -261,7 +262,9 @@ int rt_group_root_strip(rt_group* g);
 int rt_group_strip_device(rt_group* g, int i);
 /* The link model rt_group_balance plans with when strips copy into the root (distinct devices or
  * forced copies): GB/s per link and into the root.  0 (the default) = measured by the next
- * rt_group_balance (each non-root strip's copy alone, then all at once) and kept. */
+ * rt_group_balance (each non-root strip's copy alone, then all at once) and kept.  The first
+ * balance round plans the render only (its cost profile is not in ms yet); the gather-aware plan
+ * and its root strip come from the second round on, so rounds >= 2. */
 int rt_group_set_link_model(rt_group* g, double link_gbps, double ingest_gbps);
 int rt_group_link_model(rt_group* g, double* link_gbps, double* ingest_gbps);
 /* Rescale row_cost so every strip's total equals its measured time (row shape kept). */

@@ -18,7 +18,9 @@
 // up over the strips.  Strip bounds are cost-balanced (rt_group_balance): one probe frame with
 // per-row work counters, then calibration passes that time each strip and rescale the profile
 // (rt_plan_strips / rt_calibrate_row_cost, the host-only planner also used by the
-// torch.distributed path in real_time_ray_tracer_amd/dist.py).
+// torch.distributed path in real_time_ray_tracer_amd/dist.py).  When strips copy into the root
+// device, the later passes plan with the copies (rt_plan_strips_gather): the bounds and the root
+// strip, the one rendered on devices[0] in place, minimise max(render, per-link copy, ingest).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
