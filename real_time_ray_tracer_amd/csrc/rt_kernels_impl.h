@@ -889,10 +889,11 @@ __device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* 
       ar = P.bg.x; ag = P.bg.y; ab = P.bg.z;
       stop = true;
     } else {
-      float4 att = col[ind];
+      // (ABL 9, timing ablation with ABL 5's single segment: the shading without its table loads)
+      float4 att = ABL == 9 ? make_float4(0.5f, 0.5f, 0.5f, 0.0f) : col[ind];
       f3 curr = pos + t * dir;
       int id = (ALLSPH && !PL) ? SHAPE_SPHERE : __float_as_int(geo2[ind].w);
-      f3 nn = shape_normal(tab[ind], id, curr);
+      f3 nn = ABL == 9 ? normalize(curr) : shape_normal(tab[ind], id, curr);
       if (lit) {
         f3 l = normalize(light - curr);
         float spec = pow500(gclamp(dot(normalize(l - dir), nn), 0.0f, 1.0f));
@@ -901,7 +902,7 @@ __device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* 
       } else {
         ar = att.x * 0.06f; ag = att.y * 0.06f; ab = att.z * 0.06f;
       }
-      float refl = 1.0f - aux[ind].y;
+      float refl = ABL == 9 ? 0.0f : 1.0f - aux[ind].y;
       if (refl < 0.001f) {
         stop = true;
       } else {
@@ -936,7 +937,7 @@ __device__ __forceinline__ void hybrid_tile(const FrameParams& P, const float4* 
     bool live = active && !segment(0, t0, ind0, lit0);
     // segments 1 .. D-1: bounce rounds with the whole wave
     int rounds = 0;  // wave-uniform: the wave's cost beyond its camera rays (tile schedule)
-    for (int seg = 1; seg < (ABL == 5 ? 1 : P.D); ++seg) {
+    for (int seg = 1; seg < ((ABL == 5 || ABL == 9) ? 1 : P.D); ++seg) {
       if (__ballot(live) == 0) break;
       ++rounds;
       float t;

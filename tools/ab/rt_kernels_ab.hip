@@ -258,6 +258,7 @@ hipError_t launch_program(int program, const FrameParams& p, hipStream_t stream)
     if (a == 1) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 1>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
     else if (a == 3) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 3>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
     else if (a == 5) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 5>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
+    else if (a == 9) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 9>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
     else if (a == 6) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 6>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
     else if (a == 7) hipLaunchKernelGGL((hybrid_kernel<true, false, true, 7>), grid, dim3(kBlock), lt, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
     else if (a == 8) hipLaunchKernelGGL((hybrid_kernel<true, false, false, 7>), grid, dim3(kBlock), 0, stream, q.tile_order, q.sph, q.shapes, grid.x, q);
