@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # round 6 final evidence, part 1: PMC HBM bytes and SQ instruction counters per config on this build
 set -uo pipefail
-timeout -k 10 1500 bash tools/round_profile.sh counters r06x d c b a e p ref > gpurun_out/r06f1.log 2>&1
+timeout -k 10 1500 bash tools/round_profile.sh counters r06z d c b a e p ref > gpurun_out/r06f1.log 2>&1
 rc=$?
 echo "rc=$rc" >> gpurun_out/r06f1.log
 cat real_time_ray_tracer_amd/BUILD_INFO >> gpurun_out/r06f1.log

@@ -2,7 +2,7 @@
 # round 6 final evidence, part 2a: the GPU suite, smoke, the driver's command three times, and the
 # N = 2 gloo rehearsal of the multi-rank path (2 ranks on the one GPU, every gathered frame verified)
 set -uo pipefail
-O=gpurun_out/r06x; mkdir -p $O
+O=gpurun_out/r06z; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1
 rc=$?; tail -12 $O/gpu_tests.txt
 [ $rc -ne 0 ] && exit $rc

@@ -2,8 +2,8 @@
 # round 6 final evidence, part 2b: every config's bench line with its CPU baseline, rocprof
 # --kernel-trace --stats of the same command and the burst check; one-GPU strip estimates
 set -uo pipefail
-O=gpurun_out/r06x; mkdir -p $O
-timeout -k 10 900 bash tools/round_profile.sh bench r06x d c b a p ref > $O/bench_all.log 2>&1 || { tail -20 $O/bench_all.log; exit 1; }
+O=gpurun_out/r06z; mkdir -p $O
+timeout -k 10 900 bash tools/round_profile.sh bench r06z d c b a p ref > $O/bench_all.log 2>&1 || { tail -20 $O/bench_all.log; exit 1; }
 grep -v "^ \|amdgpu" $O/bench_all.log | tail -30
 timeout -k 10 200 python -u tools/strip_scaling.py --config d --n 8 --frames 20 --calibrate --warm-ms 300 \
   --save-profile $O/strip_scaling_d_n8.json > $O/strip_scaling_d_n8_calibrated.txt 2>&1 || exit $?
