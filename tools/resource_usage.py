@@ -2,7 +2,7 @@
 """Per-kernel register / LDS / occupancy table of the production library, from the compiler's
 kernel-resource-usage remarks (hipcc -Rpass-analysis=kernel-resource-usage, device pass only).
 
-    python tools/resource_usage.py [--ab] [> profiles/rNN_resource_usage.txt]
+    python tools/resource_usage.py [--ab] [VFLAGS ...] [> profiles/rNN_resource_usage.txt]
 
 The rocprofv3 kernel trace reports the same VGPR/SGPR/LDS fields per dispatch (its VGPR count
 is in allocation granules: arch VGPRs rounded up to 8); this table is what DESIGN.md's
@@ -33,7 +33,8 @@ def demangle(names):
 
 def main():
     ab = "--ab" in sys.argv
-    cmd = ["/opt/rocm/bin/hipcc", *FLAGS, "-x", "hip", "-c", str(AB_SRC if ab else SRC),
+    defines = [a for a in sys.argv[1:] if a != "--ab"]  # a variant's VFLAGS (-D..., -mllvm ...)
+    cmd = ["/opt/rocm/bin/hipcc", *FLAGS, *defines, "-x", "hip", "-c", str(AB_SRC if ab else SRC),
            "-o", "/dev/null", "--offload-device-only", "-Rpass-analysis=kernel-resource-usage"]
     text = subprocess.run(cmd, capture_output=True, text=True).stderr
     rows, cur = [], None
