@@ -1064,7 +1064,7 @@ enum { PRIM_HIT = 0, PRIM_MISS = 1, PRIM_EMISSIVE = 2 };
 struct BatchLds {
   int prec, sres, pstop, pkind, perm, cmask, rls, geol, total;
 };
-__host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
+__host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail, bool rls_lds = true) {
   const int TP = pool / spp > 0 ? pool / spp : 1, NS = TP * spp;
   BatchLds L{};
   L.prec = 0;                                   // [TP] float4: first-segment (normal, t) of sample 0
@@ -1074,7 +1074,7 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
   L.perm = L.pkind + 4 * ((TP + 1) & ~1);       // [64] int: live rank -> lane of the prepared batch
   L.cmask = (L.perm + 256 + 7) & ~7;            // [32] u64: primary cull mask (nobj <= 2048)
   L.rls = (L.cmask + 8 * 32 + 15) & ~15;        // [2 spp] float4: rand_buffer
-  L.geol = L.rls + 32 * spp;                    // [ntail] float4: sphere table (split tail rounds)
+  L.geol = L.rls + (rls_lds ? 32 * spp : 0);   // [ntail] float4: sphere table (split tail rounds)
   L.total = L.geol + 16 * ntail;
   return L;
 }
@@ -1092,6 +1092,14 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
 // the batched first bounce's exact tests deferred and merged over survivors with disjoint
 // pre-test masks (see the survivor loop): (d) 2.439 -> 2.414 ms, (c) 0.738 -> 0.730 ms
 // (profiles/r05z3_*); 0 = one exact pass per survivor that some lane passes (A/B builds)
+// Scenes above kTailMaxObj spheres (config (e)): the first bounce's per-ray pre-test with its rows
+// one 64-sphere word at a time in LDS, rand_buffer read from global memory to make room for them.
+// Before, every cone survivor (95 of 256 per batch at (e)) ran the exact test; the pre-test leaves
+// ~15 that some lane passes (tools/explore/b1_pairs_sim.py).  Config (e) 121.5 -> 97.3 ms per
+// launch, bit-identical (profiles/r06t_*).  0 = the exact tests on every survivor (A/B builds).
+#ifndef RT_PT_WIDE
+#define RT_PT_WIDE 1
+#endif
 #ifndef RT_B1_DEFER
 #define RT_B1_DEFER 1
 #endif
@@ -1101,7 +1109,7 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail) {
 constexpr int kAoMinWaves = RT_AO_MINW;
 template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL = false, bool B1 = false,
           int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false, bool CL = true, int DC = 0,
-          bool CLON = false>
+          bool CLON = false, bool PTW = false>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
   // CNT = false: the work counters compiled out (timed launches pass none): fewer live scalars
   unsigned long long* const cnts = CNT ? P.counters : nullptr;
@@ -1123,7 +1131,10 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   const int TP = POOL / spp > 0 ? POOL / spp : 1;
   const int lane = threadIdx.x;
   const int NS = TP * spp;
-  const BatchLds LO = batch_lds(spp, POOL, 0);
+  // PTW (scenes above kTailMaxObj spheres): the first bounce's pre-test rows one 64-sphere word at a
+  // time in LDS, the split tail rounds on the global table, and rand_buffer read from global memory
+  // (its LDS copy would not leave room for the rows at 7 waves per SIMD with spp 64)
+  const BatchLds LO = batch_lds(spp, POOL, 0, !PTW);
   char* lbase = (char*)lds;
   float4* prec = (float4*)(lbase + LO.prec);
   float* sres = (float*)(lbase + LO.sres);
@@ -1132,18 +1143,19 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   int* perm = (int*)(lbase + LO.perm);
   unsigned long long* cmask = (unsigned long long*)(lbase + LO.cmask);
   float4* rls = (float4*)(lbase + LO.rls);
-  for (int k = lane; k < 2 * spp; k += 64) rls[k] = f_rb[k];
+  if (!PTW)
+    for (int k = lane; k < 2 * spp; k += 64) rls[k] = f_rb[k];
   for (int k = lane; k < TP; k += 64) pstop[k] = -1;
   // TAIL: the sphere table in LDS (per-lane sphere indices in the split tail rounds)
   float4* geol = (float4*)(lbase + LO.geol);  // [nobj] when TAIL && nobj <= kTailMaxObj
   // split tail rounds: the sphere table in LDS up to kTailMaxObj spheres; above (TAIL instantiations
   // launched without the LDS table), per-lane reads of the global table (L1/L2-resident)
-  constexpr bool tail_lds = TAIL && PT;  // launch_batch: the LDS-table instantiations (<= kTailMaxObj) have PT
+  constexpr bool tail_lds = TAIL && PT && !PTW;  // launch_batch: the LDS-table instantiations (<= kTailMaxObj) have PT
   const bool tail_ok = TAIL;
   const float4* const tgeo = tail_lds ? geol : geo;
   // PT: the batched first bounce keeps its per-ray pre-test table in the same LDS rows, so the
   // sphere table is (re)staged only when a split tail round needs it
-  const bool pt_ok = PT && B1 && tail_lds;
+  const bool pt_ok = PT && B1 && (tail_lds || PTW);
   bool geol_valid = false;  // wave-uniform
   if (tail_lds && !pt_ok) {
     for (int k = lane; k < nobj; k += 64) geol[k] = geo[k];
@@ -1268,7 +1280,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   }
 
   const f3 cam = mk(P.cx, P.cy, P.cz);
-  const float4* rbuf = rls;
+  const float4* rbuf = PTW ? f_rb : rls;
   // live path of this lane
   bool has = false;
   int item = 0, depth = 0;
@@ -1513,7 +1525,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           if (pt_ok) {
             float4 pt;
             keep = i < nobj && bounce_cone_keep_pt(cb, geo[i], pt);
-            if (i < nobj) geol[i] = pt;
+            if (i < nobj) geol[PTW ? i - (w << 6) : i] = pt;  // (PTW: this word's rows only)
           } else {
             keep = i < nobj && !bounce_cone_misses(cb, geo[i]);
           }
@@ -1528,7 +1540,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
             geol_valid = false;
             __syncthreads();  // the pre-test rows are written
             if (ABL == 6) lap(5);
-            const float4* const qw = geol + (w << 6);  // this word's rows and spheres (fewer
+            const float4* const qw = geol + (PTW ? 0 : (w << 6));  // this word's rows and spheres (fewer
             const float4* const gw = geo + (w << 6);   // scalar address operations per survivor)
             // the row's LDS address is formed by one vector instruction from the row base held in
             // a VGPR (the compiler builds the uniform address with two scalar instructions and
@@ -2255,12 +2267,13 @@ template <int SPPC, bool PL, int DC = 0, bool CLON = false>
 inline void launch_batch(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStream_t stream, const FrameParams& q) {
   constexpr bool GT = RT_GLOBAL_TAIL;  // split tail rounds above kTailMaxObj spheres (global table)
   constexpr bool TLC = RT_TL_CLUSTERS;  // the cluster cull in the LDS-table (<= kTailMaxObj) instantiations
+  constexpr bool PTWV = RT_PT_WIDE;     // above kTailMaxObj spheres: the pre-test rows word by word
   if (q.mf_n > 0) {  // multi-frame mode-2 launch (never with counters: rt_compute_frames checks)
     g.y = (unsigned)q.mf_n;
     if (tl)
       hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, true, true, SPPC, true, false, PL, true, TLC, DC, CLON>), g, b, lds, stream, q, q.sph);
     else
-      hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, GT, true, SPPC, false, false, PL, true, true, DC, CLON>), g, b, lds, stream, q, q.sph);
+      hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, GT, true, SPPC, PTWV, false, PL, true, true, DC, CLON, PTWV>), g, b, lds, stream, q, q.sph);
     return;
   }
   if (tl && cnt)
@@ -2268,9 +2281,9 @@ inline void launch_batch(bool tl, bool cnt, dim3 g, dim3 b, size_t lds, hipStrea
   else if (tl)
     hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, true, true, SPPC, true, false, PL, false, TLC, DC, CLON>), g, b, lds, stream, q, q.sph);
   else if (cnt)
-    hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, GT, true, SPPC, false, true, PL, false, true, DC, CLON>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, GT, true, SPPC, PTWV, true, PL, false, true, DC, CLON, PTWV>), g, b, lds, stream, q, q.sph);
   else
-    hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, GT, true, SPPC, false, false, PL, false, true, DC, CLON>), g, b, lds, stream, q, q.sph);
+    hipLaunchKernelGGL((ao_batch_kernel<kAoMinWaves, true, kPool, 0, GT, true, SPPC, PTWV, false, PL, false, true, DC, CLON, PTWV>), g, b, lds, stream, q, q.sph);
 }
 
 // g-buffer layout conversion (rt_download / rt_upload_gbuffer, the host-buffer path of
@@ -2345,7 +2358,7 @@ inline hipError_t launch_production(int program, const FrameParams& p, const Fra
     const int TP = kPool / p.spp > 0 ? kPool / p.spp : 1;
     const long long pools = (npix + TP - 1) / TP;
     const bool tl = p.nobj <= kTailMaxObj;
-    const size_t psh = (size_t)batch_lds(p.spp, kPool, tl ? p.nobj : 0).total;
+    const size_t psh = (size_t)batch_lds(p.spp, kPool, tl ? p.nobj : (RT_PT_WIDE ? 64 : 0), tl || !RT_PT_WIDE).total;
     const dim3 g((unsigned)pools), b(64);
     // timed launches pass no counters: the counter code is compiled out (fewer live scalars)
     const bool cnt = p.counters || p.row_counters;

@@ -904,8 +904,11 @@ int rt_debug_fail_next_event_query(rt_ctx* c, int hip_error) {
 namespace {
 
 // Bounce-ray clusters of the AO kernel's later bounce rounds (rt_kernels_impl.h cluster_may_hit):
-// the spheres among [0, nobj) are cut into spatial groups of at most kClusterSize by recursive
-// median splits of their centres along the widest axis; each cluster is stored as (centre, R)
+// the spheres among [0, nobj) are cut into spatial groups of at most max(kClusterSize, ceil(sqrt(nobj)))
+// by recursive median splits of their centres along the widest axis (a round tests ~N/s balls and
+// the members of the few it keeps: config (e), 256 spheres, AO 120.0 -> 116.0 ms per launch with
+// groups of 16 instead of 8, 117.8 with 32; config (d), 64 spheres, 2.371 -> 2.395 ms with 16, so
+// 8 there, profiles/r06s_*); each cluster is stored as (centre, R)
 // with every member inside the ball: |c_i - centre| + |r_i| <= R (computed in double and
 // rounded up).  Spheres that would inflate a cluster (radius above 8x the median, e.g. a ground
 // sphere) and spheres with non-finite geometry are tested in every round instead (the always
@@ -924,6 +927,7 @@ int build_clusters(const float4* sph, int nobj, float4* ctab, unsigned long long
     if (std::isfinite(g.x) && std::isfinite(g.y) && std::isfinite(g.z) && std::isfinite(g.w)) radii.push_back(std::fabs(g.w));
   }
   if (radii.size() < (size_t)kClusterSize) return 0;
+  const int csize = std::max(kClusterSize, (int)std::ceil(std::sqrt((double)nobj)));
   std::nth_element(radii.begin(), radii.begin() + radii.size() / 2, radii.end());
   const double big = 8.0 * radii[radii.size() / 2];
   for (int i = 0; i < nobj; ++i) {
@@ -933,12 +937,12 @@ int build_clusters(const float4* sph, int nobj, float4* ctab, unsigned long long
     if (fin && std::fabs(g.w) <= big) small.push_back(i);
     else cmask[i >> 6] |= 1ull << (i & 63);  // always tested
   }
-  // recursive median split into groups of <= kClusterSize
+  // recursive median split into groups of <= csize
   std::vector<std::pair<int, int>> groups, work{{0, (int)small.size()}};
   while (!work.empty()) {
     auto [a, b] = work.back();
     work.pop_back();
-    if (b - a <= kClusterSize) {
+    if (b - a <= csize) {
       groups.push_back({a, b});
       continue;
     }

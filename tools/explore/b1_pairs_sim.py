@@ -92,6 +92,7 @@ def batch_masks(P, Dn, L, geo):
     st = np.sqrt(np.maximum(0.0, 1 - ct * ct))
     S = geo.shape[0]
     masks = np.zeros((B, S), np.uint64)
+    nkeep = np.zeros(B, np.int64)
     bits = (np.uint64(1) << np.arange(64, dtype=np.uint64))
     for j in range(S):
         c, r = geo[j, :3].astype(np.float64), abs(float(geo[j, 3]))
@@ -112,7 +113,8 @@ def batch_masks(P, Dn, L, geo):
         pas = ((Dn * u[:, None]).sum(2) >= K[:, None]) & L
         m = (pas * bits).sum(1, dtype=np.uint64)
         masks[:, j] = np.where(keep & keepb, m, 0)
-    return masks, keepb, L.sum(1)
+        nkeep += keep & keepb
+    return masks, keepb, L.sum(1), nkeep
 
 
 def count(masks, cap=64):
@@ -155,10 +157,11 @@ def main():
     fr.W, fr.H = W, H
     geo = fr.shapes[:fr.nobj, 0]
     rows = np.random.default_rng(a.seed).choice(H, a.rows, replace=False)
-    tot = dict(batches=0, b1=0, defer=0, packed=0, pairs=0, passing=0, live=0)
+    tot = dict(batches=0, b1=0, defer=0, packed=0, pairs=0, passing=0, live=0, kept=0)
     for y in rows:
         P, Dn, L = first_bounce_states(fr, int(y))
-        masks, keepb, nl = batch_masks(P, Dn, L, geo)
+        masks, keepb, nl, nk = batch_masks(P, Dn, L, geo)
+        tot["kept"] += int(nk.sum())
         d, p, q, ps = count(masks[keepb])
         tot["batches"] += masks.shape[0]
         tot["b1"] += int(keepb.sum())
@@ -167,7 +170,8 @@ def main():
     b = max(tot["b1"], 1)
     print(f"config {a.config}, {a.rows} rows: {tot['batches']} batches, {tot['b1']} with a first bounce, "
           f"{tot['live'] / b:.1f} live lanes each")
-    print(f"per first-bounce batch: survivors passed by some lane {tot['passing'] / b:.2f}, "
+    print(f"per first-bounce batch: cone-cull survivors {tot['kept'] / b:.2f} of {geo.shape[0]}, "
+          f"survivors passed by some lane {tot['passing'] / b:.2f}, "
           f"(ray, sphere) pairs {tot['pairs'] / b:.1f}")
     print(f"exact-test passes per batch: merged as built (RT_B1_DEFER) {tot['defer'] / b:.2f}, "
           f"packed 64-pair passes {tot['packed'] / b:.2f}")
