@@ -144,13 +144,17 @@ def test_ao_spp_variants(spp, scene):
     assert_bitwise(g.normals, s.normals, f"spp {spp} normals")
 
 
-@pytest.mark.parametrize("nobj", ["64", "100", "128", "129", "200", "63p", "127p", "150p"])
+@pytest.mark.parametrize("nobj", ["64", "100", "128", "129", "200", "63p", "127p", "150p", "200@4", "200@64", "150p@4",
+                                  "300@64"])
 def test_ao_scene_sizes(nobj):
     """Sphere counts around the kernel's 64-sphere words and the 128-object LDS table limit
-    (split tail rounds + the first bounce's per-ray pre-test table up to 128, without above);
-    "p": plus a ground plane (the plane-testing instantiations, with and without the LDS table)."""
+    (split tail rounds + the first bounce's per-ray pre-test table up to 128; above, the pre-test
+    rows one word at a time with rand_buffer read from global memory, RT_PT_WIDE); "p": plus a
+    ground plane (the plane-testing instantiations, with and without the LDS table); "@n": n spp
+    (the spp 4 and 64 instantiations; 16 otherwise)."""
     W, H = 48, 32
-    h = make_header(f"syn{nobj}", W, H, 16)
+    scene, _, spp = nobj.partition("@")
+    h = make_header(f"syn{scene}", W, H, int(spp) if spp else 16)
     for mode in (1, 2):
         g, s, img = run_both(h, W, H, mode, 2)
         assert_close(g.image, img, f"{nobj} spheres mode {mode} image")
