@@ -93,6 +93,7 @@ def batch_masks(P, Dn, L, geo):
     S = geo.shape[0]
     masks = np.zeros((B, S), np.uint64)
     nkeep = np.zeros(B, np.int64)
+    keepm = np.zeros((B, S), bool)
     bits = (np.uint64(1) << np.arange(64, dtype=np.uint64))
     for j in range(S):
         c, r = geo[j, :3].astype(np.float64), abs(float(geo[j, 3]))
@@ -114,7 +115,61 @@ def batch_masks(P, Dn, L, geo):
         m = (pas * bits).sum(1, dtype=np.uint64)
         masks[:, j] = np.where(keep & keepb, m, 0)
         nkeep += keep & keepb
-    return masks, keepb, L.sum(1), nkeep
+        keepm[:, j] = keep & keepb
+    return masks, keepb, L.sum(1), nkeep, keepm
+
+
+def build_clusters(geo, size):
+    """rt_shim.hip build_clusters: recursive median splits of the centres along the widest axis
+    into groups of <= size; (centre, R) with every member inside (float64 here)."""
+    idx = list(range(geo.shape[0]))
+    work, groups = [(0, len(idx))], []
+    while work:
+        a, b = work.pop()
+        if b - a <= size:
+            groups.append(idx[a:b])
+            continue
+        c = geo[idx[a:b], :3].astype(np.float64)
+        ax = int(np.argmax(c.max(0) - c.min(0)))
+        mid = (a + b) // 2
+        part = sorted(idx[a:b], key=lambda i: (float(geo[i, ax]), i))
+        idx[a:b] = part
+        work.append((mid, b))
+        work.append((a, mid))
+    out = []
+    for g in groups:
+        c = geo[g, :3].astype(np.float64).mean(0)
+        R = max(np.linalg.norm(geo[i, :3] - c) + abs(float(geo[i, 3])) for i in g)
+        out.append((np.array(g), c, R))
+    return out
+
+
+def cluster_pretest(P, Dn, L, geo, clusters):
+    """Per batch: the clusters whose ball some live lane's pre-test passes (the same pre-test as a
+    sphere's, on the ball inflated to R sqrt(1+1e-5) + sqrt(1e-5) Lmax + rho), and the cone-kept
+    spheres that lie in such clusters."""
+    B = P.shape[0] // 64
+    P, Dn, L = P[:B * 64].reshape(B, 64, 3), Dn[:B * 64].reshape(B, 64, 3), L[:B * 64].reshape(B, 64)
+    first = np.argmax(L, 1)
+    o = P[np.arange(B), first]
+    e2 = np.where(L, ((P - o[:, None]) ** 2).sum(2), 0).max(1)
+    rho = np.sqrt(e2) * 1.0001 + 1e-6 * np.abs(o).sum(1)
+    member_pass = np.zeros((B, geo.shape[0]), bool)
+    npass = np.zeros(B, np.int64)
+    for g, c, R in clusters:
+        v = c - o
+        Ln = np.sqrt((v ** 2).sum(1))
+        Lmax = Ln + R + rho
+        Re = R * np.sqrt(1 + 1e-5) * 1.0001 + np.sqrt(1e-5) * Lmax * 1.0001 + rho
+        sa = Re / Ln
+        near = ~(sa < 1.0)
+        ca = np.sqrt(np.maximum(0.0, 1 - sa * sa))
+        u = v / Ln[:, None]
+        K = np.where(near, -2.0, ca - 2e-5)
+        pas = (((Dn * u[:, None]).sum(2) >= K[:, None]) & L).any(1)
+        npass += pas
+        member_pass[:, g] = pas[:, None]
+    return member_pass, npass
 
 
 def count(masks, cap=64):
@@ -157,11 +212,20 @@ def main():
     fr.W, fr.H = W, H
     geo = fr.shapes[:fr.nobj, 0]
     rows = np.random.default_rng(a.seed).choice(H, a.rows, replace=False)
-    tot = dict(batches=0, b1=0, defer=0, packed=0, pairs=0, passing=0, live=0, kept=0)
+    tot = dict(batches=0, b1=0, defer=0, packed=0, pairs=0, passing=0, live=0, kept=0, ckept=0, cpass=0, nclus=0)
+    csize = max(8, int(np.ceil(np.sqrt(geo.shape[0]))))
+    clusters = build_clusters(geo, csize)
     for y in rows:
         P, Dn, L = first_bounce_states(fr, int(y))
-        masks, keepb, nl, nk = batch_masks(P, Dn, L, geo)
+        masks, keepb, nl, nk, km = batch_masks(P, Dn, L, geo)
         tot["kept"] += int(nk.sum())
+        mp, npc = cluster_pretest(P, Dn, L, geo, clusters)
+        kept_sph = (masks != 0)  # (survivors some lane passes are a subset of the cone-kept ones)
+        # cone-kept spheres in passing clusters: recount the cone keep per sphere from batch_masks' nk
+        tot["cpass"] += int(npc[keepb].sum())
+        tot["nclus"] += len(clusters) * int(keepb.sum())
+        tot["ckept"] += int((mp[keepb] & km[keepb]).sum())
+        tot["miss"] = tot.get("miss", 0) + int((kept_sph[keepb] & ~mp[keepb]).sum())
         d, p, q, ps = count(masks[keepb])
         tot["batches"] += masks.shape[0]
         tot["b1"] += int(keepb.sum())
@@ -173,6 +237,9 @@ def main():
     print(f"per first-bounce batch: cone-cull survivors {tot['kept'] / b:.2f} of {geo.shape[0]}, "
           f"survivors passed by some lane {tot['passing'] / b:.2f}, "
           f"(ray, sphere) pairs {tot['pairs'] / b:.1f}")
+    print(f"clusters of <= {csize}: {len(clusters)}, of which some lane's ball pre-test passes {tot['cpass'] / b:.2f} "
+          f"per batch; cone survivors inside them {tot['ckept'] / b:.2f} (loop iterations after the cluster pre-test); "
+          f"passing survivors outside them (must be 0): {tot.get('miss', 0)}")
     print(f"exact-test passes per batch: merged as built (RT_B1_DEFER) {tot['defer'] / b:.2f}, "
           f"packed 64-pair passes {tot['packed'] / b:.2f}")
 
