@@ -212,6 +212,14 @@ static bool ab_launch_ao(const FrameParams& p, FrameParams& q, hipStream_t strea
     if (variant == 108) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 11, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
     if (variant == 109) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 12, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
     if (variant == 110) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 13, true, true, 16, true, false, false, false, true, 20, true>), g, b, ps, stream, q, q.sph);
+  } else if ((variant == 193 || variant == 196 || variant == 198) && !tl && p.spp == 64 && p.nplanes == 0 &&
+             q.ncl > 0 && p.D == 20) {
+    // section clocks of config (e)'s production instantiation (above kTailMaxObj spheres: the
+    // word-by-word pre-test, rand_buffer from global memory): 193 as 93, 196 as 96, 198 as 98
+    const size_t pw = (size_t)batch_lds(64, kPool, 64, false).total;
+    if (variant == 193) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 3, true, true, 64, true, true, false, false, true, 20, true, true>), g, b, pw, stream, q, q.sph);
+    if (variant == 196) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 6, true, true, 64, true, true, false, false, true, 20, true, true>), g, b, pw, stream, q, q.sph);
+    if (variant == 198) hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 8, true, true, 64, true, true, false, false, true, 20, true, true>), g, b, pw, stream, q, q.sph);
   } else if (variant == 91)
     hipLaunchKernelGGL((ao_batch_kernel<7, true, kPool, 1>), g, b, psh, stream, q, q.sph);
   else if (variant == 92)

@@ -6,6 +6,7 @@
     python tools/sections.py --config d --variant 96   # the first bounce split into cull / survivors / shade
     python tools/sections.py --config d --variant 97   # event counts: first-bounce survivors, bounce-round tails
     python tools/sections.py --config d --variant 98   # full bounce rounds and split tail rounds apart
+    python tools/sections.py --config e --variant 193  # (e)'s instantiation (196, 198 as 96, 98)
 """
 import argparse
 import os
@@ -52,7 +53,7 @@ def main():
               f"the passing lanes {v[2] / max(v[0], 1):.3f}; lanes passing per iteration {v[3] / max(v[0], 1):.2f}")
         print(f"bounce rounds: {v[6]} sphere iterations, any live lane del >= 0 in {v[7] / max(v[6], 1):.3f}")
         return
-    if a.variant == "98":
+    if a.variant in ("98", "198"):
         names = ["cull setup", "prepare (primary + first shade)", "hand-out / regeneration", "full bounce rounds",
                  "first bounce (batched) + combine + stores", "split tail rounds"]
         v = [c[k] for k in keys]
@@ -61,7 +62,7 @@ def main():
             print(f"{n:42s} {x / 1e9:9.3f} Gclk  {100 * x / tot:5.1f}%")
         print(f"full rounds {v[6]}, split tail rounds {v[7]}")
         return
-    if a.variant == "96":
+    if a.variant in ("96", "196"):
         names = ["cull setup", "prepare (primary + first shade)", "hand-out / regeneration", "bounce test + shade",
                  "combine + stores", "first bounce: cone + cull", "first bounce: survivor tests",
                  "first bounce: shade"]
