@@ -1085,13 +1085,12 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail, b
 // and slot buffers, the image by the launch's last frame only.
 // CL: the bounce-ray cluster cull of the later bounce rounds (P.ncl > 0); without it the rounds
 // test every sphere.
+// PTW (with PT, above kTailMaxObj spheres): the first bounce's pre-test rows one 64-sphere word at a
+// time, the split tail rounds on the global table, rand_buffer read from global memory (RT_PT_WIDE).
 // waves per SIMD the production AO kernel is compiled for (its register budget: 7 -> 72 VGPRs)
 #ifndef RT_AO_MINW
 #define RT_AO_MINW 7
 #endif
-// the batched first bounce's exact tests deferred and merged over survivors with disjoint
-// pre-test masks (see the survivor loop): (d) 2.439 -> 2.414 ms, (c) 0.738 -> 0.730 ms
-// (profiles/r05z3_*); 0 = one exact pass per survivor that some lane passes (A/B builds)
 // Scenes above kTailMaxObj spheres (config (e)): the first bounce's per-ray pre-test with its rows
 // one 64-sphere word at a time in LDS, rand_buffer read from global memory to make room for them.
 // Before, every cone survivor (95 of 256 per batch at (e)) ran the exact test; the pre-test leaves
@@ -1100,6 +1099,9 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail, b
 #ifndef RT_PT_WIDE
 #define RT_PT_WIDE 1
 #endif
+// the batched first bounce's exact tests deferred and merged over survivors with disjoint
+// pre-test masks (see the survivor loop): (d) 2.439 -> 2.414 ms, (c) 0.738 -> 0.730 ms
+// (profiles/r05z3_*); 0 = one exact pass per survivor that some lane passes (A/B builds)
 #ifndef RT_B1_DEFER
 #define RT_B1_DEFER 1
 #endif
