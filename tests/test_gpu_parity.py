@@ -98,14 +98,18 @@ def test_mode_parity_small(scene, mode):
 
 
 @pytest.mark.parametrize("chunks", [(2, 3), (37, 1)])
-@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 5])
 def test_compute_frames_equals_frame_by_frame(mode, chunks):
     """rt_compute_frames (the C++ frame loop; sequential frames go in batches of up to 32 device
     header copies with one upload) renders the same frames as FrameDriver.compute() called once
     per frame: g-buffer ring, image, frame slot and the updated header, bit for bit — across a
-    batch boundary too, and with one more per-frame call after the loop (the state it leaves)."""
+    batch boundary too, and with one more per-frame call after the loop (the state it leaves).
+    "mode 5": mode 2 on 200 spheres, so the multi-frame launches take the above-128-sphere
+    instantiations (the word-by-word pre-test, per-frame rand_buffer read from global memory)."""
     W, H, spp = 48, 32, 4
-    h = make_header("syn16p" if mode == 4 else "syn16", W, H, spp)
+    scene = {4: "syn16p", 5: "syn200"}.get(mode, "syn16")
+    mode = 2 if mode == 5 else mode
+    h = make_header(scene, W, H, spp)
     n = sum(chunks) + 1
     outs = []
     for many in (False, True, "one launch per frame"):
