@@ -1105,6 +1105,14 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail, b
 #ifndef RT_B1_DEFER
 #define RT_B1_DEFER 1
 #endif
+// The batched first bounce at wave issue priority 1 (s_setprio), every other phase at 0: among
+// the ready waves of a SIMD, those in the first bounce's latency-bound survivor loop issue first.
+// Per launch (d) 2.382 -> 2.349 ms, (c) 0.707 -> 0.698, (e) 93.0 -> 91.4; pipelined (d) frames
+// 2.172 -> 2.141 ms over three alternating rounds; images identical.  The later bounce rounds at
+// priority 1 too: level or worse; all of prepare(): worse pipelined (profiles/r06pm_*).
+#ifndef RT_B1_PRIO
+#define RT_B1_PRIO 1
+#endif
 #ifndef RT_B1_CREAD
 #define RT_B1_CREAD 1
 #endif
@@ -1484,6 +1492,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
       const unsigned long long lm1 = __ballot(live);
       if (lm1 != 0 && __popcll(lm1) >= P.b1_min) {
         lap(1);
+        if (RT_B1_PRIO) __builtin_amdgcn_s_setprio(1);
         const ConeB cb = bounce_cone(live, bpos, bdir, lm1);
         float t = -1.0f;
         int ind = -1;
@@ -1610,6 +1619,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
           }
         }
         if (RT_B1_DEFER && ru != 0) flush();
+        if (RT_B1_PRIO) __builtin_amdgcn_s_setprio(0);
         if (ABL == 7) { tsec[4] += 1; tsec[5] += (unsigned long long)__popcll(lm1); }
         if (live) {
           if (PL) plane_pass(P, bpos, bdir, 0.0001f, t, ind);
