@@ -1113,6 +1113,14 @@ __host__ __device__ constexpr BatchLds batch_lds(int spp, int pool, int ntail, b
 #ifndef RT_B1_PRIO
 #define RT_B1_PRIO 1
 #endif
+// The pool's start (its LDS set-up, the rand_buffer copy and the primary cone cull: two dependent
+// global-load round trips) at priority 1 as well, so a new wave's loads issue ahead of the
+// resident waves' arithmetic: per launch (d) 2.441 -> 2.407 ms, (c) 0.714 -> 0.703, pipelined (d)
+// frames 2.144-2.154 -> 2.139-2.148 ms on top of RT_B1_PRIO; the split tail rounds at priority 1
+// instead: per launch -1.8% but pipelined frames +0.3% (profiles/r06px_*).
+#ifndef RT_START_PRIO
+#define RT_START_PRIO 1
+#endif
 #ifndef RT_B1_CREAD
 #define RT_B1_CREAD 1
 #endif
@@ -1121,6 +1129,7 @@ template <int MINW, bool LAZY = true, int POOL = kPool, int ABL = 0, bool TAIL =
           int SPPC = 0, bool PT = false, bool CNT = true, bool PL = false, bool MF = false, bool CL = true, int DC = 0,
           bool CLON = false, bool PTW = false>
 __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const float4* __restrict__ geo) {
+  if (RT_START_PRIO) __builtin_amdgcn_s_setprio(1);
   // CNT = false: the work counters compiled out (timed launches pass none): fewer live scalars
   unsigned long long* const cnts = CNT ? P.counters : nullptr;
   unsigned long long* const rowc = CNT ? P.row_counters : nullptr;
@@ -1259,6 +1268,7 @@ __global__ __launch_bounds__(64, MINW) void ao_batch_kernel(FrameParams P, const
   }
   __syncthreads();
   lap(0);
+  if (RT_START_PRIO) __builtin_amdgcn_s_setprio(0);
 
   if (LAZY && ncull == 0) {
     // Empty frustum: every primary ray of the pool provably misses every sphere, so each
